@@ -1,0 +1,136 @@
+"""Pin the CPU oracle (oracle/oracle.py) against the golden vectors that
+tests/golden/make_golden.py produced by running the reference's own code.
+
+Tolerances (written per check):
+  * cars CBF rows: bit-exact (same fp32 op order as rcbf_sac/diff_cbf_qp.py:268-357)
+  * unicycle CBF rows: <= 2e-6 relative -- the only difference is torch's SLEEF
+    fp32 cos/sin vs the oracle's correctly rounded cos/sin (1 ulp on theta;
+    with torch's cos/sin substituted the oracle rows are bit-exact)
+  * safe action: <= 1e-5 relative to max(1,|u|) (north-star bar is 1e-4)
+  * gradients: <= 1e-5 relative (the reference's grad runs through fp32 rows)
+  * env states: bit-exact for cars; unicycle <= 1e-14 relative (BLAS ddot FMA)
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b)))) if a.size else 0.0
+
+
+@pytest.mark.parametrize("tag", ["prior", "rand"])
+def test_cars_layer(golden, tag):
+    d = golden("cars_layer")
+    g = float(d["gamma_b"])
+    P, q, G, h = O.cars_build_diff(d[tag + "_x"], d[tag + "_u"], d[tag + "_mu"], d[tag + "_sigma"], g)
+    assert np.array_equal(G, d[tag + "_G"]) and np.array_equal(h, d[tag + "_h"])
+    assert np.array_equal(P, d[tag + "_P"])
+    fin, aux = O.safe_action_diff("SimulatedCars", d[tag + "_x"], d[tag + "_u"], d[tag + "_mu"], d[tag + "_sigma"], g)
+    assert np.array_equal(aux["Gn"], d[tag + "_Gn"]) and np.array_equal(aux["hn"], d[tag + "_hn"])
+    assert (aux["status"] == 0).all()
+    assert rel(aux["z"], d[tag + "_z"]) < 1e-10
+    assert rel(fin, d[tag + "_final"]) < 1e-5
+    grad, _ = O.safe_action_diff_grad("SimulatedCars", d[tag + "_x"], d[tag + "_u"], d[tag + "_mu"],
+                                      d[tag + "_sigma"], g, d[tag + "_w"])
+    assert rel(grad, d[tag + "_grad_u"]) < 1e-5
+
+
+@pytest.mark.parametrize("k", [3, 5])
+@pytest.mark.parametrize("tag", ["prior", "rand"])
+def test_unicycle_layer(golden, k, tag):
+    d = golden(f"unicycle{k}_layer")
+    g = float(d["gamma_b"])
+    args = (d[tag + "_x"], d[tag + "_u"], d[tag + "_mu"], d[tag + "_sigma"], g)
+    P, q, G, h = O.unicycle_build_diff(*args, d["hazards"], l_p=float(d["l_p"]))
+    # a 1-ulp cos/sin difference moves h through gamma*h_s^3 by ~1e-6 relative
+    assert rel(h, d[tag + "_h"]) < 2e-6
+    assert rel(G, d[tag + "_G"]) < 1e-6
+    fin, aux = O.safe_action_diff("Unicycle", *args, hazards=d["hazards"], l_p=float(d["l_p"]))
+    assert (aux["status"] == 0).all()
+    assert rel(fin, d[tag + "_final"]) < 1e-5
+    grad, _ = O.safe_action_diff_grad("Unicycle", *args, d[tag + "_w"], hazards=d["hazards"], l_p=float(d["l_p"]))
+    assert rel(grad, d[tag + "_grad_u"]) < 1e-5
+
+
+def test_cascade(golden):
+    c = golden("cascade")
+    P, G, h = O.cars_build_cascade(c["cars_x"], c["cars_u"], 20.0)
+    assert rel(G, c["cars_G"]) < 1e-15 and rel(h, c["cars_h"]) < 1e-14
+    Gn, hn, _ = O.normalize_rows(G, h)
+    z, lam, act, st = O.qp_exact(np.diag(P), Gn, hn)
+    assert (st == 0).all() and rel(z[:, :1], c["cars_usafe"]) < 1e-9
+    P, G, h = O.unicycle_build_cascade(c["uni_x"], c["uni_u"], c["uni_mu"], c["uni_sigma"], 40.0, 3.0, O.UNI["hazards"])
+    assert rel(G, c["uni_G"]) < 1e-14 and rel(h, c["uni_h"]) < 1e-14
+    Gn, hn, _ = O.normalize_rows(G, h)
+    z, lam, act, st = O.qp_exact(np.diag(P), Gn, hn)
+    assert (st == 0).all() and rel(z[:, :2], c["uni_usafe"]) < 1e-8
+
+
+def test_cars_env_traj(golden):
+    d = golden("env_traj")
+    for e in range(d["cars_noise"].shape[0]):
+        x, t, st = O.cars_reset(d["cars_noise"][e:e + 1])
+        assert np.array_equal(x[0], d["cars_state"][e, 0])
+        for k in range(300):
+            x, t, st, obs, r, c, dn = O.cars_step(x, t, st, d["cars_actions"][e, k][None])
+            assert np.array_equal(x[0], d["cars_state"][e, k + 1])
+            assert np.array_equal(obs[0], d["cars_obs"][e, k + 1])
+            assert t[0] == d["cars_t"][e, k + 1]
+            # reference squares an np.float32 SCALAR (powf): <= 1 fp32 ulp from a*a
+            assert abs(r[0] - d["cars_reward"][e, k]) <= 2 * np.spacing(np.float32(abs(r[0])))
+            assert c[0] == d["cars_cost"][e, k] and dn[0] == d["cars_done"][e, k]
+
+
+def test_unicycle_env_traj(golden):
+    d = golden("env_traj")
+    x, ld, st = O.uni_reset(1)
+    assert np.array_equal(O.uni_obs(x)[0], d["uni_obs"][0])
+    for k in range(1000):
+        x, ld, st, obs, r, c, dn, gm = O.uni_step(x, ld, st, d["uni_actions"][k][None])
+        assert rel(x[0], d["uni_state"][k + 1]) < 1e-14
+        assert rel(obs[0], d["uni_obs"][k + 1]) < 1e-13
+        assert abs(r[0] - d["uni_reward"][k]) < 1e-13
+        assert c[0] == d["uni_cost"][k] and dn[0] == d["uni_done"][k]
+    n_goal = 0
+    for e in range(d["unir_x0"].shape[0]):
+        x = d["unir_x0"][e:e + 1].copy(); ld = O.uni_goal_dist(x); st = d["unir_step0"][e:e + 1]
+        for k in range(d["unir_actions"].shape[1]):
+            x, ld, st, obs, r, c, dn, gm = O.uni_step(x, ld, st, d["unir_actions"][e, k][None])
+            assert rel(x[0], d["unir_state"][e, k + 1]) < 1e-13
+            assert rel(obs[0], d["unir_obs"][e, k + 1]) < 1e-12
+            assert c[0] == d["unir_cost"][e, k] and dn[0] == d["unir_done"][e, k] and gm[0] == d["unir_goal"][e, k]
+            n_goal += int(gm[0])
+            if dn[0]:
+                break
+    assert n_goal >= 1 and d["unir_cost"].sum() > 0
+
+
+def test_dynamics_glue(golden):
+    d = golden("dynamics")
+    for nm, mode in (("cars", "SimulatedCars"), ("uni", "Unicycle")):
+        assert np.array_equal(O.get_state(mode, d[nm + "_obs"]), d[nm + "_state_np"])
+        assert np.array_equal(O.get_state_f32(mode, d[nm + "_obs32"]), d[nm + "_state_t"])
+        m, s = O.predict_disturbance_prior(mode, d[nm + "_obs"].shape[0])
+        assert np.array_equal(m.astype(np.float32), d[nm + "_mean"])
+        assert np.array_equal(s.astype(np.float32), d[nm + "_sigma"])
+        nx = O.predict_next_state_prior(mode, d[nm + "_state_np"], d[nm + "_u"], d.get(nm + "_t"))
+        assert np.array_equal(nx, d[nm + "_next"])
+
+
+def test_closed_loop_config1(golden):
+    """Config 1: hand controller + CascadeCBFLayer(gamma_b=20,k_d=3) + cars env,
+    300 steps (envs/simulated_cars_env.py:161-228 without the plotting)."""
+    cl = golden("closed_loop_cars")
+    x, t, st = O.cars_reset(cl["noise"])
+    for k in range(300):
+        s = O.get_state("SimulatedCars", O.cars_obs(x))
+        un = cl["u_nom"][k]
+        P, G, h = O.cars_build_cascade(s, un[None], 20.0)
+        Gn, hn, _ = O.normalize_rows(G, h)
+        z, lam, act, stt = O.qp_exact(np.diag(P), Gn, hn)
+        assert rel(z[:, :1], cl["u_safe"][k]) < 1e-8
+        x, t, st, obs, r, c, dn = O.cars_step(x, t, st, un[None] + cl["u_safe"][k][None])
+        assert np.array_equal(x[0], cl["state"][k + 1])
