@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""Headline benchmark: safe env steps/s (dynamics + CBF-QP) at batch 65536.
+
+A "step" is one fused safe step of every env of the batch
+(rcbf_safe_step: get_state(obs32) -> CBFQPLayer.get_safe_action (build,
+row-normalise, fp64 QP, clamp) -> env.step -> obs/reward/cost/done,
+auto-reset) with the env state, u_RL and outputs resident in HBM.  u_RL is
+synthetic (uniform in the action box, like the reference's warm-up policy,
+main.py:88-92), mean/sigma are the DynamicsModel prior (dynamics.py:381-384).
+
+Multi-GPU: one process per GPU (torchrun), each GPU owns `--batch` envs
+(weak scaling, no collective on the data path; RCCL only for the barrier and
+the max-over-ranks time).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "sac-rcbf_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+# Algorithmic HBM bytes of one env-step of rcbf_safe_step ("bytes per step"):
+#   cars:     read  x 80 + t 8 + step 4 + u_RL 4                         =  96
+#             write x 80 + t 8 + step 4 + obs 40 + u 4 + r 4 + c 4 + done 1 = 145
+#   unicycle: read  x 24 + last_dist 8 + step 4 + u_RL 8                 =  44
+#             write x 24 + ld 8 + step 4 + obs 28 + u 8 + r 4 + c 4 + done 1 + goal 1 = 82
+BYTES_PER_STEP = {"SimulatedCars": 96 + 145, "Unicycle": 44 + 82}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--env", default="SimulatedCars", choices=["SimulatedCars", "Unicycle"])
+    ap.add_argument("--hazards", type=int, default=3, help="unicycle hazard count")
+    ap.add_argument("--solver", default="active_set", choices=["active_set", "pdipm"])
+    ap.add_argument("--graph-steps", type=int, default=50, help="fused steps per captured hipGraph")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extra", action="store_true", help="also time the K-step rollout kernel and big batches")
+    return ap.parse_args()
+
+
+def largest_divisor_le(n, cap):
+    for s in range(min(n, cap), 0, -1):
+        if n % s == 0:
+            return s
+    return 1
+
+
+def cpu_baseline(env_name, hazards, seconds):
+    """The numpy oracle's fused step (oracle/oracle.py) on the host, bounded
+    to ~`seconds`: build + exact QP + clamp + env step per env."""
+    from oracle import oracle as O
+    B = 16384
+    rng = np.random.default_rng(0)
+    if env_name == "SimulatedCars":
+        x, t, st = O.cars_reset(rng.normal(0, 0.5, B))
+        mu, sg = O.predict_disturbance_prior("SimulatedCars", B)
+        mu, sg = mu.astype(np.float32), sg.astype(np.float32)
+    else:
+        x, ld, st = O.uni_reset(B)
+        hz = O.UNI["hazards"][:hazards]
+        mu, sg = np.zeros((B, 3), np.float32), np.full((B, 3), 0.2, np.float32)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        if env_name == "SimulatedCars":
+            u = rng.uniform(-1, 1, (B, 1)).astype(np.float32)
+            s32 = O.get_state_f32("SimulatedCars", O.cars_obs(x).astype(np.float32))
+            fin, _ = O.safe_action_diff("SimulatedCars", s32, u, mu, sg, 20.0)
+            x, t, st, *_ = O.cars_step(x, t, st, fin)
+        else:
+            u = rng.uniform(-1, 1, (B, 2)).astype(np.float32)
+            s32 = O.get_state_f32("Unicycle", O.uni_obs(x).astype(np.float32))
+            fin, _ = O.safe_action_diff("Unicycle", s32, u, mu, sg, 20.0, hazards=hz)
+            x, ld, st, *_ = O.uni_step(x, ld, st, fin, hazards=hz)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 1000:
+            break
+    return {"value": round(n * B / el, 1), "unit": "safe env steps/s", "cores": 1, "kind": "port",
+            "sample": f"numpy oracle fused step, {n} steps x {B} envs ({el:.1f} s), 1 thread"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from rcbf_amd import _lib
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+
+    class LArgs:
+        cuda = True
+
+    B = args.batch
+    solver = _lib.SOLVER_PDIPM if args.solver == "pdipm" else _lib.SOLVER_ACTIVE_SET
+    if args.env == "SimulatedCars":
+        env = BatchedSimulatedCarsEnv(B, device=dev, seed=1234, env_offset=rank * B)
+    else:
+        from oracle.oracle import UNI  # constants only
+        env = BatchedUnicycleEnv(B, device=dev, seed=1234, env_offset=rank * B,
+                                 hazards_locations=UNI["hazards"][:args.hazards])
+    layer = CBFQPLayer(env, LArgs(), gamma_b=20.0, solver=solver)
+    S = largest_divisor_le(args.steps, args.graph_steps)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
+    pool = [(torch.rand(B, env.n_u, device=dev, generator=gen) * 2 - 1).contiguous() for _ in range(S)]
+    outs = env.make_outputs()
+    if args.env == "SimulatedCars":
+        outs["goal_met"] = None
+
+    def steps(n, off=0):
+        for j in range(n):
+            env.safe_step(pool[(off + j) % S], layer, outputs=outs)
+
+    # warmup (eager), then capture S fused steps into one hipGraph
+    steps(max(args.warmup, 1))
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        steps(2)  # warm the side stream before capture
+    torch.cuda.current_stream(dev).wait_stream(s)
+    with torch.cuda.graph(graph):
+        steps(S)
+    for _ in range(2):
+        graph.replay()
+    torch.cuda.synchronize()
+    env.check_failures()
+
+    reps = args.steps // S
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(reps):
+        graph.replay()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # per fused-step launch, on the launch stream
+    env.check_failures()
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        k = torch.tensor([kern_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        kern_ms = float(k.item())
+
+    total_steps = world * B * args.steps
+    value = total_steps / el
+    bps = BYTES_PER_STEP[args.env]
+    achieved = B * bps / (kern_ms * 1e-3) / 1e9
+    extra = {}
+    if args.extra and rank == 0:
+        extra = extra_measurements(env, layer, dev, args)
+    rec = {
+        "metric": "safe env steps/sec (dynamics+CBF-QP) at batch 65536, 1/2/4/8 MI355X",
+        "value": round(value, 1),
+        "unit": "safe env steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 rows / f64 QP / f64 env",
+        "data": "synthetic (u_RL ~ U[-1,1], prior mean/sigma, seeded resets)",
+        "config": {"workload": f"{args.env} fused safe step (rcbf_safe_step), non-diff CBF-QP, "
+                               f"{'3-hazard ' if args.env == 'Unicycle' and args.hazards == 3 else ''}"
+                               f"batch {B} envs per GPU, {args.solver} fp64 QP, hipGraph of {S} steps",
+                   "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
+                   "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "k_safe_step", "bytes_per_launch": B * bps,
+                     "kernel_ms": round(kern_ms, 5)},
+    }
+    if extra:
+        rec["extra"] = extra
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(args.env, args.hazards, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def extra_measurements(env, layer, dev, args):
+    """Secondary numbers (not `value`): the K-step rollout kernel (state in
+    registers across steps) and the fused step at a batch beyond the 256 MiB
+    Infinity Cache."""
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv
+    out = {}
+    K = 100
+    u = (torch.rand(K, env.num_envs, env.n_u, device=dev) * 2 - 1).contiguous()
+    env.rollout(u, layer)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    env.rollout(u, layer)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    out["rollout_K100_steps_per_s"] = round(env.num_envs * K / (ms * 1e-3), 1)
+    if args.env == "SimulatedCars":
+        Bb = 4 * 1024 * 1024
+        big = BatchedSimulatedCarsEnv(Bb, device=dev, seed=5)
+        ub = (torch.rand(Bb, 1, device=dev) * 2 - 1).contiguous()
+        o = big.make_outputs()
+        o["goal_met"] = None
+        for _ in range(3):
+            big.safe_step(ub, layer, outputs=o)
+        torch.cuda.synchronize()
+        e0.record()
+        n = 20
+        for _ in range(n):
+            big.safe_step(ub, layer, outputs=o)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / n
+        out["batch_4M_steps_per_s"] = round(Bb / (ms * 1e-3), 1)
+        out["batch_4M_hbm_GBs"] = round(Bb * BYTES_PER_STEP["SimulatedCars"] / (ms * 1e-3) / 1e9, 1)
+    return out
+
+
+if __name__ == "__main__":
+    main()

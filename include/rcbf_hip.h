@@ -1,0 +1,195 @@
+/*
+ * rcbf_hip.h -- C-ABI of librcbf_hip.so, the MI355X (gfx950) batched safe-env
+ * step of SAC-RCBF: control-affine dynamics + RCBF safety-layer QP.
+ *
+ * Every entry point replaces one reference interface (paths relative to the
+ * reference repo yemam3/SAC-RCBF); the Python mirror in
+ * sac-rcbf_amd/rcbf_amd/ binds them through ctypes.
+ *
+ * Conventions
+ *   - All array arguments are CALLER-OWNED DEVICE pointers (PyTorch allocates;
+ *     the library never allocates on the hot path).  Layouts are the
+ *     reference's row-major tensors: x (B, n_s), u (B, n_u), G (B, m, n) ...
+ *   - `stream` is the HIP stream to launch on (torch's current stream);
+ *     every call is asynchronous, stateless and re-entrant (no globals), so
+ *     one process per GPU or several streams are safe, and calls can be
+ *     captured into a hipGraph.
+ *   - Return value: 0 on success, otherwise a hipError_t value or one of the
+ *     RCBF_E_* argument errors below.  Nothing throws across the ABI.
+ *   - Per-QP solver status is written to device arrays (status_out) and
+ *     OR-ed into an optional device word (fail_flag, bit (1<<status)) so the
+ *     host can raise the reference's Exception('QP Failed to solve')
+ *     (rcbf_sac/diff_cbf_qp.py:141-143) after a single 4-byte read.
+ *   - Nullable pointers are marked [nullable].
+ */
+#ifndef RCBF_HIP_H
+#define RCBF_HIP_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RCBF_ABI_VERSION 2
+
+/* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
+#define RCBF_MODE_SIMULATED_CARS 0
+#define RCBF_MODE_UNICYCLE 1
+
+/* constraint formulations */
+#define RCBF_FORM_DIFF 0    /* CBFQPLayer, rcbf_sac/diff_cbf_qp.py (fp32 rows, fp64 QP)  */
+#define RCBF_FORM_CASCADE 1 /* CascadeCBFLayer, rcbf_sac/cbf_qp.py (fp64 rows, fp64 QP) */
+
+/* QP solvers */
+#define RCBF_SOLVER_ACTIVE_SET 0 /* Goldfarb-Idnani dual active set, fp64 (quadprog's algorithm, exact) */
+#define RCBF_SOLVER_PDIPM 1      /* primal-dual interior point, fp64 (qpth's algorithm family)        */
+
+/* per-QP status codes */
+#define RCBF_QP_OK 0
+#define RCBF_QP_MAX_ITER 1
+#define RCBF_QP_INFEASIBLE 2
+#define RCBF_QP_NONFINITE 3
+
+/* argument errors (returned instead of a hipError_t) */
+#define RCBF_E_BAD_MODE 1001
+#define RCBF_E_BAD_SHAPE 1002
+#define RCBF_E_NULL 1003
+
+#define RCBF_MAX_HAZARDS 8
+
+/* Layer + env constants.  Mirrors the ctor arguments of CBFQPLayer
+ * (diff_cbf_qp.py:12-42) / CascadeCBFLayer (cbf_qp.py:7-27) and the env
+ * attributes they read (kp, k_brake, safe_action_space, hazards_*).  */
+typedef struct rcbf_params {
+    int32_t mode;        /* RCBF_MODE_*                                   */
+    int32_t formulation; /* RCBF_FORM_*                                   */
+    int32_t num_hazards; /* unicycle: len(env.hazards_locations) <= 8     */
+    int32_t solver;      /* RCBF_SOLVER_*                                  */
+    int32_t max_iter;    /* solver iteration cap (0 -> default)           */
+    int32_t _pad;
+    double gamma_b;      /* gamma of the barrier certificate              */
+    double k_d;          /* confidence multiplier (Cascade unicycle only) */
+    double l_p;          /* look-ahead distance (unicycle)                */
+    double kp, k_brake;  /* cars gains (simulated_cars_env.py:25-26)      */
+    double u_min[2], u_max[2]; /* env.safe_action_space.low/high          */
+    double hazards_radius;
+    double hazards_xy[2 * RCBF_MAX_HAZARDS];
+    double eps;          /* PDIPM stopping tolerance (qpth eps, default 1e-4 -> we use 1e-10) */
+} rcbf_params;
+
+/* ---------------------------------------------------------------------- */
+/* CBF-QP layer                                                            */
+/* ---------------------------------------------------------------------- */
+
+/* CBFQPLayer.get_cbf_qp_constraints (diff_cbf_qp.py:146-379), fp32.
+ * x, mu, sigma (B, n_s); u_rl (B, n_u).  mu/sigma [nullable] -> the
+ * DynamicsModel prior (dynamics.py:381-384: mean 0, sigma MAX_STD).
+ * Outputs P (B,n,n), q (B,n), G (B,m,n), h (B,m) with n = n_u+1 and
+ * m = num_cbfs + 2 n_u, row order as the reference. */
+int rcbf_build(const rcbf_params* prm, int64_t B, const float* x, const float* u_rl,
+               const float* mu, const float* sigma, float* P_out, float* q_out,
+               float* G_out, float* h_out, hipStream_t stream);
+
+/* CascadeCBFLayer.get_cbf_qp_constraints (cbf_qp.py:55-240), fp64, batched. */
+int rcbf_build_f64(const rcbf_params* prm, int64_t B, const double* x, const double* u_nom,
+                   const double* mu, const double* sigma, double* P_out, double* q_out,
+                   double* G_out, double* h_out, hipStream_t stream);
+
+/* CBFQPLayer.solve_qp + cbf_layer (diff_cbf_qp.py:81-144): optional row
+ * normalisation (normalize=1: rows of [G h] divided by their max-abs entry,
+ * :103-106), then  min 1/2 z'Pz + q'z  s.t.  Gz <= h  in fp64 for a general
+ * SPD P (n <= 3, m <= 16).  z_out fp32 (the reference's .float()).
+ * lam_out [nullable] (B,m) fp64 multipliers; status_out [nullable] (B,);
+ * fail_flag [nullable] one device int32, OR-ed with (1<<status) on failure. */
+int rcbf_qp_solve(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P,
+                  const float* q, const float* G, const float* h, int32_t normalize,
+                  float* z_out, double* lam_out, int32_t* status_out, int32_t* fail_flag,
+                  hipStream_t stream);
+
+/* CBFQPLayer.get_safe_action (diff_cbf_qp.py:44-79), fused in one kernel:
+ * build -> normalise -> fp64 QP -> .float() -> clamp(u_rl + u_qp, u_min, u_max).
+ * mu/sigma [nullable] -> prior.  u_out (B, n_u) fp32. */
+int rcbf_safe_action(const rcbf_params* prm, int64_t B, const float* x, const float* u_rl,
+                     const float* mu, const float* sigma, float* u_out, int32_t* status_out,
+                     int32_t* fail_flag, hipStream_t stream);
+
+/* Backward of rcbf_safe_action w.r.t. u_rl (the only input the reference's
+ * autograd reaches, sac_cbf.py:147-158): implicit-KKT derivative of the QP on
+ * its active set (what qpth's QPFunction.backward approximates), through the
+ * row normaliser and the clamp.  Recomputes the forward in-kernel (no saved
+ * tensors).  grad_u (B,n_u) in, grad_u_rl (B,n_u) out. */
+int rcbf_safe_action_backward(const rcbf_params* prm, int64_t B, const float* x,
+                              const float* u_rl, const float* mu, const float* sigma,
+                              const float* grad_u, float* grad_u_rl, hipStream_t stream);
+
+/* CascadeCBFLayer.get_u_safe (cbf_qp.py:29-53), fp64 batched: build ->
+ * normalise -> exact QP.  Returns u_qp only (caller adds u_nom, no clamp). */
+int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom,
+                        const double* x, const double* mu, const double* sigma,
+                        double* u_safe_out, int32_t* status_out, int32_t* fail_flag,
+                        hipStream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Environments (batched, device-resident, fp64 state like the numpy envs) */
+/* ---------------------------------------------------------------------- */
+/* Per-env state:  x (B, n_s) f64 = env.state;  aux (B,) f64 = env.t (cars)
+ * or env.last_goal_dist (unicycle);  step (B,) i32 = env.episode_step;
+ * episode (B,) u32 = reset counter keying the per-env counter-based RNG.  */
+
+/* SimulatedCarsEnv.reset (simulated_cars_env.py:108-125) / UnicycleEnv.reset
+ * (unicycle_env.py:125-143) for the envs selected by mask [nullable: all].
+ * noise [nullable] (B,) f64 injects the cars' N(0,0.5) velocity draw; when
+ * null it comes from a Philox4x32-10 counter RNG keyed by (seed, env_offset + env
+ * index, episode): env_offset is the global index of env 0 of this shard, so a
+ * sharded run draws exactly what the unsharded run draws.
+ * obs_out [nullable] (B, n_o) f32. */
+int rcbf_env_reset(const rcbf_params* prm, int64_t B, const uint8_t* mask, const double* noise,
+                   uint64_t seed, int64_t env_offset, double* x, double* aux, int32_t* step,
+                   uint32_t* episode, float* obs_out, hipStream_t stream);
+
+/* env.step(action) (simulated_cars_env.py:38-106, unicycle_env.py:46-111),
+ * batched.  action (B, n_u), fp32 (action_f64 = 0) or fp64 (action_f64 = 1);
+ * the cars reward is computed in the action's dtype like the reference.
+ * Outputs: obs64_out [nullable] (B,n_o) f64, obs_out [nullable] (B,n_o) f32,
+ * reward (B,) f64, cost (B,) f64, done (B,) u8, goal_met [nullable] (B,) u8.
+ * auto_reset=1 resets finished envs in place (obs = post-reset obs). */
+int rcbf_env_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step,
+                  uint32_t* episode, const void* action, int32_t action_f64, double* obs64_out,
+                  float* obs_out, double* reward, double* cost, uint8_t* done, uint8_t* goal_met,
+                  int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream);
+
+/* The fused safe step -- the hot path measured by bench.py:
+ *   obs32 = float(obs(x)); state = get_state(obs32) (dynamics.py:190-232);
+ *   mean,sigma = prior or given; u = CBFQPLayer.get_safe_action(state, u_rl,
+ *   mean, sigma); env.step(u) with optional auto-reset; obs32 of the new state.
+ * All in one launch, one env per lane, env state read and written in place.
+ * u_out (B,n_u) f32 safe action; reward/cost (B,) f32; done (B,) u8;
+ * goal_met [nullable]; status_out [nullable]; fail_flag [nullable]. */
+int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step,
+                   uint32_t* episode, const float* u_rl, const float* mu, const float* sigma,
+                   float* obs_out, float* u_out, float* reward, float* cost, uint8_t* done,
+                   uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag,
+                   int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream);
+
+/* K fused safe steps in ONE launch with the env state held in registers
+ * (a pre-sampled u_rl (K, B, n_u), e.g. the reference's warm-up phase that
+ * samples action_space uniformly, main.py:88-92).  Per-step outputs are
+ * reduced per env: reward_sum, cost_sum (B,) f32, episodes finished (B,) i32.
+ * obs_out [nullable] (B,n_o) f32 final observation. */
+int rcbf_safe_rollout(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux,
+                      int32_t* step, uint32_t* episode, const float* u_rl, float* obs_out,
+                      float* reward_sum, float* cost_sum, int32_t* n_done, int32_t* fail_flag,
+                      uint64_t seed, int64_t env_offset, hipStream_t stream);
+
+/* ---------------------------------------------------------------------- */
+const char* rcbf_version(void);
+int32_t rcbf_abi_version(void);
+/* sizeof(rcbf_params) as compiled, for binding checks (no GPU needed). */
+int32_t rcbf_params_size(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RCBF_HIP_H */

@@ -1,0 +1,1117 @@
+// rcbf_device.hpp -- device building blocks of the MI355X batched safe-env step.
+//
+// One env / one QP per lane.  Everything an env needs lives in VGPRs for the
+// whole step: its state, its CBF constraint rows, the QP iterate and the
+// active set.  The QP is tiny (n <= 3 variables, m <= 12 rows), so there is
+// no MFMA shape here; the kernels are HBM/latency bound and the solvers are
+// written branch-light with compile-time loop bounds so every small array
+// stays in registers (no scratch).
+//
+// Numerics mirror the reference's dtypes and operation order:
+//   * CBFQPLayer rows: fp32, every elementwise op rounded (torch CPU), no FMA
+//     contraction (`#pragma clang fp contract(off)` in those functions)
+//   * the QP: fp64 (diff_cbf_qp.py:139 casts to double)
+//   * the envs: fp64 (numpy), again without contraction
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rcbf_hip.h"
+
+namespace rcbf {
+
+constexpr double kInf = __builtin_huge_val();
+
+// ---------------------------------------------------------------------------
+// small fixed-size linear algebra (compile-time sizes -> registers)
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ double dotd(const double* a, const double* b) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) s = fma(a[k], b[k], s);
+    return s;
+}
+
+// Solve S r = w for SPD S (N x N, lower triangle used) by LDL^T without
+// pivoting.  Padded (inactive) slots carry an identity block.  Returns false
+// on a non-positive pivot.
+template <int N>
+__device__ __forceinline__ bool ldl_solve(double S[N][N], const double* w, double* r) {
+    double L[N][N];
+    double D[N];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        double d = S[j][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k] * D[k];
+        ok = ok && (d > 0.0);
+        D[j] = d;
+        double inv = 1.0 / d;
+#pragma unroll
+        for (int i = j + 1; i < N; ++i) {
+            double v = S[i][j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k] * D[k];
+            L[i][j] = v * inv;
+        }
+    }
+    double y[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        double v = w[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) v -= L[i][k] * y[k];
+        y[i] = v;
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        double v = y[i] / D[i];
+#pragma unroll
+        for (int k = i + 1; k < N; ++k) v -= L[k][i] * r[k];
+        r[i] = v;
+    }
+    return ok;
+}
+
+// Solve A x = b (N x N general, rows of A = active constraint normals) by
+// Gaussian elimination with partial pivoting, fully unrolled.
+template <int N>
+__device__ __forceinline__ void gauss_solve(double A[N][N], double* b, double* x) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+        // pivot: swap the largest |A[r][c]|, r >= c, into row c (select-based)
+#pragma unroll
+        for (int r = c + 1; r < N; ++r) {
+            bool sw = fabs(A[r][c]) > fabs(A[c][c]);
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                double a = A[c][k], bb = A[r][k];
+                A[c][k] = sw ? bb : a;
+                A[r][k] = sw ? a : bb;
+            }
+            double a = b[c], bb = b[r];
+            b[c] = sw ? bb : a;
+            b[r] = sw ? a : bb;
+        }
+        double inv = 1.0 / A[c][c];
+#pragma unroll
+        for (int r = c + 1; r < N; ++r) {
+            double f = A[r][c] * inv;
+#pragma unroll
+            for (int k = c; k < N; ++k) A[r][k] -= f * A[c][k];
+            b[r] -= f * b[c];
+        }
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        double v = b[i];
+#pragma unroll
+        for (int k = i + 1; k < N; ++k) v -= A[i][k] * x[k];
+        x[i] = v / A[i][i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Strictly convex QP   min 1/2 z'Pz + q'z   s.t.  G z <= h
+// P is given by its inverse (diagonal or full, n <= 3).
+// ---------------------------------------------------------------------------
+template <int N, bool DIAG>
+struct PMat {
+    double P[N][N];     // P      (only the diagonal when DIAG)
+    double Pinv[N][N];  // P^-1   (only the diagonal when DIAG)
+    __device__ __forceinline__ void inv_apply(const double* v, double* o) const {
+        if (DIAG) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) o[i] = Pinv[i][i] * v[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < N; ++i) o[i] = dotd<N>(Pinv[i], v);
+        }
+    }
+    __device__ __forceinline__ void apply(const double* v, double* o) const {
+        if (DIAG) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) o[i] = P[i][i] * v[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < N; ++i) o[i] = dotd<N>(P[i], v);
+        }
+    }
+};
+
+template <int N>
+__device__ __forceinline__ void pmat_set_diag(PMat<N, true>& pm, const double* d) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        pm.P[i][i] = d[i];
+        pm.Pinv[i][i] = 1.0 / d[i];
+    }
+}
+
+// Full SPD P: invert by Gauss-Jordan on the unit vectors (n <= 3).
+template <int N>
+__device__ __forceinline__ void pmat_set_full(PMat<N, false>& pm, const double Pin[N][N]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        double A[N][N], e[N], col[N];
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+#pragma unroll
+            for (int c = 0; c < N; ++c) A[r][c] = Pin[r][c];
+            e[r] = (r == j) ? 1.0 : 0.0;
+        }
+        gauss_solve<N>(A, e, col);
+#pragma unroll
+        for (int r = 0; r < N; ++r) pm.Pinv[r][j] = col[r];
+    }
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+#pragma unroll
+        for (int c = 0; c < N; ++c) pm.P[r][c] = Pin[r][c];
+}
+
+template <int N, int M>
+struct QPResult {
+    double z[N];
+    double lam[M];     // multipliers (0 for inactive rows)
+    uint32_t active;   // bit r set <=> row r in the final active set
+    int nact;
+    int status;        // RCBF_QP_*
+    int iters;
+};
+
+// Active rows are tracked in N slots (|A| <= n for a strictly convex QP with
+// independent active normals).  Slot s holds a copy of its row.
+template <int N>
+struct ActiveSet {
+    double g[N][N];
+    double h[N];
+    double lam[N];
+    int idx[N];
+    int n;
+};
+
+// Equality-constrained re-solve on the active set ("polish"): the exact KKT
+// point for the final active set, recomputed from scratch so the GI step
+// accumulation error does not survive.  Vertex case (|A| = n) solves
+// G_A z = h_A directly -- well conditioned after row normalisation even when
+// the multipliers are ~1e7 (Cascade unicycle, P = diag(10,1e-4,1e7)).
+template <int N, bool DIAG>
+__device__ __forceinline__ void polish(const PMat<N, DIAG>& pm, const double* x0, const double* q,
+                                       ActiveSet<N>& A, double* z) {
+    if (A.n == N) {
+        double GA[N][N], hA[N];
+#pragma unroll
+        for (int s = 0; s < N; ++s) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) GA[s][k] = A.g[s][k];
+            hA[s] = A.h[s];
+        }
+        gauss_solve<N>(GA, hA, z);
+        // lam_A = -G_A^{-T} (P z + q)
+        double Pz[N], rhs[N], GT[N][N];
+        pm.apply(z, Pz);
+#pragma unroll
+        for (int k = 0; k < N; ++k) rhs[k] = -(Pz[k] + q[k]);
+#pragma unroll
+        for (int r = 0; r < N; ++r)
+#pragma unroll
+            for (int c = 0; c < N; ++c) GT[r][c] = A.g[c][r];
+        double lam[N];
+        gauss_solve<N>(GT, rhs, lam);
+#pragma unroll
+        for (int s = 0; s < N; ++s) A.lam[s] = lam[s];
+        return;
+    }
+    // |A| < n: lam = S^-1 (G_A x0 - h_A), z = x0 - P^-1 G_A' lam  (+1 refinement)
+    double PG[N][N];  // P^-1 g_s
+#pragma unroll
+    for (int s = 0; s < N; ++s) pm.inv_apply(A.g[s], PG[s]);
+    double S[N][N], w[N], lam[N];
+#pragma unroll
+    for (int s = 0; s < N; ++s) {
+#pragma unroll
+        for (int t = 0; t < N; ++t) {
+            bool in = (s < A.n) && (t < A.n);
+            S[s][t] = in ? dotd<N>(A.g[s], PG[t]) : (s == t ? 1.0 : 0.0);
+        }
+        w[s] = (s < A.n) ? dotd<N>(A.g[s], x0) - A.h[s] : 0.0;
+    }
+    double S2[N][N];
+#pragma unroll
+    for (int s = 0; s < N; ++s)
+#pragma unroll
+        for (int t = 0; t < N; ++t) S2[s][t] = S[s][t];
+    ldl_solve<N>(S2, w, lam);
+    double res[N], corr[N];
+#pragma unroll
+    for (int s = 0; s < N; ++s) res[s] = w[s] - dotd<N>(S[s], lam);
+#pragma unroll
+    for (int s = 0; s < N; ++s)
+#pragma unroll
+        for (int t = 0; t < N; ++t) S2[s][t] = S[s][t];
+    ldl_solve<N>(S2, res, corr);
+#pragma unroll
+    for (int s = 0; s < N; ++s) lam[s] = (s < A.n) ? lam[s] + corr[s] : 0.0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        double acc = x0[k];
+#pragma unroll
+        for (int s = 0; s < N; ++s) acc -= PG[s][k] * lam[s];
+        z[k] = acc;
+    }
+#pragma unroll
+    for (int s = 0; s < N; ++s) A.lam[s] = lam[s];
+}
+
+// Goldfarb-Idnani dual active-set method (the algorithm of quadprog, which
+// the reference's CascadeCBFLayer calls at cbf_qp.py:276), in a re-solve
+// form suited to n <= 3: the active-set Schur system S = G_A P^-1 G_A' is
+// rebuilt and LDL-solved at each step instead of carrying QR updates.
+// Rows are type R (fp32 normalised rows of the diff layer, or fp64).
+// Starting from the unconstrained minimum, the most violated row is added;
+// a partial step drops the blocking active row; every step keeps dual
+// feasibility, and the method terminates at the unique optimum.
+template <int N, int M, bool DIAG, typename R>
+__device__ __forceinline__ void gi_solve(const PMat<N, DIAG>& pm, const double* q, const R (*G)[N],
+                                         const R* h, int max_iter, QPResult<N, M>& out) {
+    double x0[N];
+    pm.inv_apply(q, x0);
+#pragma unroll
+    for (int k = 0; k < N; ++k) x0[k] = -x0[k];
+    double x[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) x[k] = x0[k];
+    ActiveSet<N> A;
+    A.n = 0;
+#pragma unroll
+    for (int s = 0; s < N; ++s) {
+        A.idx[s] = -1;
+        A.lam[s] = 0.0;
+        A.h[s] = 0.0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) A.g[s][k] = 0.0;
+    }
+    uint32_t amask = 0;
+    int status = RCBF_QP_MAX_ITER;
+    int it = 0;
+    bool finite = true;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        finite = finite && isfinite((double)h[r]);
+#pragma unroll
+        for (int k = 0; k < N; ++k) finite = finite && isfinite((double)G[r][k]);
+    }
+    if (!finite) {
+        status = RCBF_QP_NONFINITE;
+        it = max_iter;
+    }
+    while (it < max_iter) {
+        // (1) most violated inactive row
+        int p = -1;
+        double vbest = 0.0;
+        double gp[N], hp = 0.0;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            double gr[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) gr[k] = (double)G[r][k];
+            double v = dotd<N>(gr, x) - (double)h[r];
+            double tol = 1e-12 * (1.0 + fabs((double)h[r]));
+            bool take = !((amask >> r) & 1u) && (v > tol) && (v > vbest);
+            vbest = take ? v : vbest;
+            p = take ? r : p;
+#pragma unroll
+            for (int k = 0; k < N; ++k) gp[k] = take ? gr[k] : gp[k];
+            hp = take ? (double)h[r] : hp;
+        }
+        if (p < 0) {
+            status = RCBF_QP_OK;
+            break;
+        }
+        double lamp = 0.0;
+        // (2) step loop for the violated row p
+        bool added = false;
+        while (it < max_iter) {
+            ++it;
+            double Pg[N];
+            pm.inv_apply(gp, Pg);
+            double PG[N][N];
+#pragma unroll
+            for (int s = 0; s < N; ++s) pm.inv_apply(A.g[s], PG[s]);
+            double S[N][N], w[N], r[N];
+#pragma unroll
+            for (int s = 0; s < N; ++s) {
+#pragma unroll
+                for (int t = 0; t < N; ++t) {
+                    bool in = (s < A.n) && (t < A.n);
+                    S[s][t] = in ? dotd<N>(A.g[s], PG[t]) : (s == t ? 1.0 : 0.0);
+                }
+                w[s] = (s < A.n) ? dotd<N>(A.g[s], Pg) : 0.0;
+            }
+            ldl_solve<N>(S, w, r);
+            // primal direction z = -P^-1 (g_p - G_A' r)
+            double zdir[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                double acc = Pg[k];
+#pragma unroll
+                for (int s = 0; s < N; ++s) acc -= PG[s][k] * ((s < A.n) ? r[s] : 0.0);
+                zdir[k] = -acc;
+            }
+            double gz = dotd<N>(gp, zdir);
+            double gPg = dotd<N>(gp, Pg);
+            double t2 = kInf;
+            if (A.n < N && gz < -1e-13 * gPg) t2 = (dotd<N>(gp, x) - hp) / (-gz);
+            double t1 = kInf;
+            int kdrop = -1;
+#pragma unroll
+            for (int s = 0; s < N; ++s) {
+                bool cand = (s < A.n) && (r[s] > 1e-14);
+                double tt = cand ? A.lam[s] / r[s] : kInf;
+                bool better = cand && (tt < t1);
+                t1 = better ? tt : t1;
+                kdrop = better ? s : kdrop;
+            }
+            if (t1 == kInf && t2 == kInf) {
+                status = RCBF_QP_INFEASIBLE;
+                it = max_iter;
+                break;
+            }
+            double t = fmin(t1, t2);
+            if (t2 != kInf) {
+#pragma unroll
+                for (int k = 0; k < N; ++k) x[k] = fma(t, zdir[k], x[k]);
+            }
+#pragma unroll
+            for (int s = 0; s < N; ++s) A.lam[s] = (s < A.n) ? fmax(A.lam[s] - t * r[s], 0.0) : 0.0;
+            lamp += t;
+            if (t2 <= t1) {
+                // full step: p joins the active set in slot A.n
+#pragma unroll
+                for (int s = 0; s < N; ++s) {
+                    bool here = (s == A.n);
+#pragma unroll
+                    for (int k = 0; k < N; ++k) A.g[s][k] = here ? gp[k] : A.g[s][k];
+                    A.h[s] = here ? hp : A.h[s];
+                    A.lam[s] = here ? lamp : A.lam[s];
+                    A.idx[s] = here ? p : A.idx[s];
+                }
+                A.n += 1;
+                amask |= (1u << p);
+                added = true;
+                break;
+            }
+            // partial step: drop the blocking row kdrop (shift slots down)
+            int dropped = A.idx[0];
+#pragma unroll
+            for (int s = 0; s < N; ++s) dropped = (s == kdrop) ? A.idx[s] : dropped;
+            amask &= ~(1u << dropped);
+#pragma unroll
+            for (int s = 0; s + 1 < N; ++s) {
+                bool sh = (s >= kdrop);
+#pragma unroll
+                for (int k = 0; k < N; ++k) A.g[s][k] = sh ? A.g[s + 1][k] : A.g[s][k];
+                A.h[s] = sh ? A.h[s + 1] : A.h[s];
+                A.lam[s] = sh ? A.lam[s + 1] : A.lam[s];
+                A.idx[s] = sh ? A.idx[s + 1] : A.idx[s];
+            }
+            A.n -= 1;
+            A.idx[N - 1] = -1;
+            A.lam[N - 1] = 0.0;
+        }
+        (void)added;
+    }
+    if (status == RCBF_QP_OK) {
+        polish<N, DIAG>(pm, x0, q, A, x);
+    }
+    bool okf = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        out.z[k] = x[k];
+        okf = okf && isfinite(x[k]);
+    }
+    if (!okf && status == RCBF_QP_OK) status = RCBF_QP_NONFINITE;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        double l = 0.0;
+#pragma unroll
+        for (int s = 0; s < N; ++s) l = (s < A.n && A.idx[s] == r) ? A.lam[s] : l;
+        out.lam[r] = l;
+    }
+    out.active = amask;
+    out.nact = A.n;
+    out.status = status;
+    out.iters = it;
+}
+
+// Primal-dual interior point (Mehrotra predictor-corrector), the algorithm
+// family of qpth (diff_cbf_qp.py:139; OptNet, Amos & Kolter 2017): slack s,
+// multipliers lam, Newton steps on the n x n normal equations
+//   (P + G' D G) dx = -rx + G' rs - G' D rz,   D = lam / s,
+// qpth's initialisation (s, lam shifted to >= 1), its 0.999 fraction to the
+// boundary and sigma = (mu_aff / mu)^3, per-QP best-iterate tracking and its
+// stop rule (resid < eps, or notImprovedLim steps without improvement).
+// Followed by the same exact active-set polish as the GI path (rows with
+// lam > s), so the returned z is the KKT point of the identified set.
+template <int N, int M, bool DIAG, typename R>
+__device__ __forceinline__ void pdipm_solve(const PMat<N, DIAG>& pm, const double* q, const R (*G)[N],
+                                            const R* h, int max_iter, double eps, QPResult<N, M>& out) {
+    double Gd[M][N], hd[M];
+    bool finite = true;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        hd[r] = (double)h[r];
+        finite = finite && isfinite(hd[r]);
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            Gd[r][k] = (double)G[r][k];
+            finite = finite && isfinite(Gd[r][k]);
+        }
+    }
+    double x[N], s[M], lam[M];
+    // initial point: solve the KKT with D = I (qpth's d = ones), rx = q, rz = -h
+    {
+        double H[N][N];
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                double acc = DIAG ? (i == j ? pm.P[i][i] : 0.0) : pm.P[i][j];
+#pragma unroll
+                for (int r = 0; r < M; ++r) acc += Gd[r][i] * Gd[r][j];
+                H[i][j] = acc;
+            }
+        // (P + G'G) x = -q + G'h   (rs = 0, rz = -h)
+        double rhs[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double acc = -q[i];
+#pragma unroll
+            for (int r = 0; r < M; ++r) acc += Gd[r][i] * hd[r];
+            rhs[i] = acc;
+        }
+        ldl_solve<N>(H, rhs, x);
+        double smin = kInf, lmin = kInf;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            double gx = dotd<N>(Gd[r], x);
+            // ds = -rz - G dx with rz = -h  ->  s = h - G x ; lam = D(G x - h) = -s
+            s[r] = hd[r] - gx;
+            lam[r] = gx - hd[r];
+            smin = fmin(smin, s[r]);
+            lmin = fmin(lmin, lam[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            if (smin < 0.0) s[r] -= smin - 1.0;
+            if (lmin < 0.0) lam[r] -= lmin - 1.0;
+        }
+    }
+    double best_res = kInf, bx[N], bs[M], bl[M];
+#pragma unroll
+    for (int k = 0; k < N; ++k) bx[k] = x[k];
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        bs[r] = s[r];
+        bl[r] = lam[r];
+    }
+    int not_improved = 0;
+    int it = 0;
+    int status = finite ? RCBF_QP_MAX_ITER : RCBF_QP_NONFINITE;
+    const int not_improved_lim = 10;  // diff_cbf_qp.py:107
+    for (; finite && it < max_iter; ++it) {
+        // residuals
+        double rx[N], rz[M], Px[N];
+        pm.apply(x, Px);
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            double acc = Px[k] + q[k];
+#pragma unroll
+            for (int r = 0; r < M; ++r) acc += Gd[r][k] * lam[r];
+            rx[k] = acc;
+        }
+        double sz = 0.0, zr = 0.0;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            rz[r] = dotd<N>(Gd[r], x) + s[r] - hd[r];
+            sz += s[r] * lam[r];
+            zr += rz[r] * rz[r];
+        }
+        double mu = fabs(sz / M);
+        double res = sqrt(zr) + sqrt(dotd<N>(rx, rx)) + M * mu;
+        if (res < best_res) {
+            best_res = res;
+            not_improved = 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) bx[k] = x[k];
+#pragma unroll
+            for (int r = 0; r < M; ++r) {
+                bs[r] = s[r];
+                bl[r] = lam[r];
+            }
+        } else {
+            ++not_improved;
+        }
+        if (best_res < eps) {
+            status = RCBF_QP_OK;
+            break;
+        }
+        if (not_improved >= not_improved_lim) {
+            status = RCBF_QP_OK;  // qpth returns its best iterate here too
+            break;
+        }
+        // normal-equation matrix H = P + G' D G
+        double d[M], H[N][N];
+#pragma unroll
+        for (int r = 0; r < M; ++r) d[r] = lam[r] / s[r];
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) {
+                double acc = DIAG ? (i == j ? pm.P[i][i] : 0.0) : pm.P[i][j];
+#pragma unroll
+                for (int r = 0; r < M; ++r) acc += Gd[r][i] * d[r] * Gd[r][j];
+                H[i][j] = acc;
+                H[j][i] = acc;
+            }
+        // affine direction: rs = lam
+        double dx[N], ds[M], dl[M], rhs[N];
+        auto kkt = [&](const double* rs_, double* dx_, double* ds_, double* dl_) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                double acc = -rx[k];
+#pragma unroll
+                for (int r = 0; r < M; ++r) acc += Gd[r][k] * (rs_[r] - d[r] * rz[r]);
+                rhs[k] = acc;
+            }
+            double Hc[N][N];
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+#pragma unroll
+                for (int j = 0; j < N; ++j) Hc[i][j] = H[i][j];
+            ldl_solve<N>(Hc, rhs, dx_);
+#pragma unroll
+            for (int r = 0; r < M; ++r) {
+                ds_[r] = -rz[r] - dotd<N>(Gd[r], dx_);
+                dl_[r] = -rs_[r] - d[r] * ds_[r];
+            }
+        };
+        double rs[M];
+#pragma unroll
+        for (int r = 0; r < M; ++r) rs[r] = lam[r];
+        kkt(rs, dx, ds, dl);
+        // step to the boundary
+        double a_aff = 1.0;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            if (dl[r] < 0.0) a_aff = fmin(a_aff, -lam[r] / dl[r]);
+            if (ds[r] < 0.0) a_aff = fmin(a_aff, -s[r] / ds[r]);
+        }
+        double t3 = 0.0;
+#pragma unroll
+        for (int r = 0; r < M; ++r) t3 += (s[r] + a_aff * ds[r]) * (lam[r] + a_aff * dl[r]);
+        double sig = t3 / sz;
+        sig = sig * sig * sig;
+        // corrector: rs = (-mu sig + ds_aff dl_aff) / s, rx = rz = 0, added
+        double dxc[N], dsc[M], dlc[M];
+        {
+            double rx0[N], rz0[M];
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                rx0[k] = rx[k];
+                rx[k] = 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < M; ++r) {
+                rz0[r] = rz[r];
+                rz[r] = 0.0;
+                rs[r] = (-mu * sig + ds[r] * dl[r]) / s[r];
+            }
+            kkt(rs, dxc, dsc, dlc);
+#pragma unroll
+            for (int k = 0; k < N; ++k) rx[k] = rx0[k];
+#pragma unroll
+            for (int r = 0; r < M; ++r) rz[r] = rz0[r];
+        }
+        double alpha = 1.0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) dx[k] += dxc[k];
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            ds[r] += dsc[r];
+            dl[r] += dlc[r];
+        }
+        double amax = kInf;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            if (dl[r] < 0.0) amax = fmin(amax, -lam[r] / dl[r]);
+            if (ds[r] < 0.0) amax = fmin(amax, -s[r] / ds[r]);
+        }
+        // qpth's get_step: no blocking direction -> step 1 (then x0.999)
+        if (amax == kInf) amax = 1.0;
+        alpha = fmin(1.0, 0.999 * amax);
+#pragma unroll
+        for (int k = 0; k < N; ++k) x[k] += alpha * dx[k];
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            s[r] += alpha * ds[r];
+            lam[r] += alpha * dl[r];
+        }
+    }
+    // active-set polish on {r : lam_r > s_r} (at most N rows, largest lam first)
+    ActiveSet<N> A;
+    A.n = 0;
+    uint32_t amask = 0;
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) {
+        A.idx[sl] = -1;
+        A.lam[sl] = 0.0;
+        A.h[sl] = 0.0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) A.g[sl][k] = 0.0;
+    }
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) {
+        int pick = -1;
+        double lb = 0.0;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            bool c = !((amask >> r) & 1u) && (bl[r] > bs[r]) && (bl[r] > lb);
+            lb = c ? bl[r] : lb;
+            pick = c ? r : pick;
+        }
+        if (pick >= 0) {
+#pragma unroll
+            for (int r = 0; r < M; ++r) {
+                if (r == pick) {
+#pragma unroll
+                    for (int k = 0; k < N; ++k) A.g[sl][k] = Gd[r][k];
+                    A.h[sl] = hd[r];
+                }
+            }
+            A.idx[sl] = pick;
+            A.n = sl + 1;
+            amask |= 1u << pick;
+        }
+    }
+    double z[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) z[k] = bx[k];
+    if (finite) {
+        double x0[N];
+        pm.inv_apply(q, x0);
+#pragma unroll
+        for (int k = 0; k < N; ++k) x0[k] = -x0[k];
+        double zp[N];
+        polish<N, DIAG>(pm, x0, q, A, zp);
+        // accept the polish only if it is primal and dual feasible
+        bool ok = true;
+#pragma unroll
+        for (int r = 0; r < M; ++r) ok = ok && (dotd<N>(Gd[r], zp) - hd[r] <= 1e-9 * (1.0 + fabs(hd[r])));
+#pragma unroll
+        for (int sl = 0; sl < N; ++sl) ok = ok && (sl >= A.n || A.lam[sl] >= -1e-9);
+#pragma unroll
+        for (int k = 0; k < N; ++k) z[k] = ok ? zp[k] : z[k];
+    }
+    bool okf = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        out.z[k] = z[k];
+        okf = okf && isfinite(z[k]);
+    }
+    if (!okf) status = RCBF_QP_NONFINITE;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        double l = 0.0;
+#pragma unroll
+        for (int sl = 0; sl < N; ++sl) l = (sl < A.n && A.idx[sl] == r) ? A.lam[sl] : l;
+        out.lam[r] = l;
+    }
+    out.active = amask;
+    out.nact = A.n;
+    out.status = status;
+    out.iters = it;
+}
+
+template <int N, int M, bool DIAG, typename R>
+__device__ __forceinline__ void qp_solve(int solver, const PMat<N, DIAG>& pm, const double* q,
+                                         const R (*G)[N], const R* h, int max_iter, double eps,
+                                         QPResult<N, M>& out) {
+    if (solver == RCBF_SOLVER_PDIPM)
+        pdipm_solve<N, M, DIAG, R>(pm, q, G, h, max_iter > 0 ? max_iter : 50, eps > 0 ? eps : 1e-10, out);
+    else
+        gi_solve<N, M, DIAG, R>(pm, q, G, h, max_iter > 0 ? max_iter : 4 * (M + N) + 8, out);
+}
+
+// ---------------------------------------------------------------------------
+// Row normalisation  (diff_cbf_qp.py:103-106 / cbf_qp.py:270-273)
+//   N_r = max(|G_r|_inf, |h_r|);  G_r /= N_r;  h_r /= N_r
+// argmax_is_h records whether torch.max picked the h entry (first maximum
+// wins, as torch.max(dim) returns the first maximal index) -- the backward
+// routes dN/dh only through that entry.
+// ---------------------------------------------------------------------------
+template <int N, int M, typename T>
+__device__ __forceinline__ void normalize_rows(T (*G)[N], T* h, T* Nrm, bool* argmax_is_h) {
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        T mx = fabs(G[r][0]);
+#pragma unroll
+        for (int k = 1; k < N; ++k) mx = fmax(mx, fabs(G[r][k]));
+        T ah = fabs(h[r]);
+        bool ish = ah > mx;
+        T nr = ish ? ah : mx;
+        Nrm[r] = nr;
+        if (argmax_is_h) argmax_is_h[r] = ish;
+#pragma unroll
+        for (int k = 0; k < N; ++k) G[r][k] = G[r][k] / nr;
+        h[r] = h[r] / nr;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CBF constraint builders
+// ---------------------------------------------------------------------------
+// SimulatedCars, CBFQPLayer form (diff_cbf_qp.py:268-357, actuators 362-377).
+// fp32, torch's elementwise order; mu is not used by the reference.
+// sig5/7/9 = sigma[:, 5], [:, 7], [:, 9] (fD_x at the odd entries, :298-299).
+__device__ __forceinline__ void cars_rows_diff(const rcbf_params& prm, const float* xs, float u,
+                                               float sig5, float sig7, float sig9, float (*G)[2],
+                                               float* h) {
+#pragma clang fp contract(off)
+    const float kp = (float)prm.kp, kb = (float)prm.k_brake;
+    float p0 = xs[0], p1 = xs[2], p2 = xs[4], p3 = xs[6], p4 = xs[8];
+    float v0 = xs[1], v1 = xs[3], v2 = xs[5], v3 = xs[7], v4 = xs[9];
+    (void)v0;
+    float a1 = kp * (30.0f - v1), a2 = kp * (30.0f - v2), a4 = kp * (30.0f - v4);
+    float d01 = p0 - p1, d12 = p1 - p2, d24 = p2 - p4;
+    a1 = a1 - (kb * d01) * (d01 < 6.0f ? 1.0f : 0.0f);
+    a2 = a2 - (kb * d12) * (d12 < 6.0f ? 1.0f : 0.0f);
+    const float a3 = 0.0f;  // car 4's acceleration is the control (:289)
+    a4 = a4 - (kb * d24) * (d24 < 13.0f ? 1.0f : 0.0f);
+    float e23 = p2 - p3, e43 = p4 - p3;
+    float h13 = 0.5f * ((e23 * e23) - 12.25f);
+    float h15 = 0.5f * ((e43 * e43) - 12.25f);
+    float h13d = (p3 - p2) * (v3 - v2);
+    float h15d = (p3 - p4) * (v3 - v4);
+    float c4 = v2 - v3, c5 = p2 - p3, c6 = v3 - v2, c7 = p3 - p2;
+    float Lff13 = ((c4 * v2 + c5 * a2) + c6 * v3) + c7 * a3;
+    float LfD13 = fabsf(c5) * sig5 + fabsf(c7) * sig7;
+    float e6 = v3 - v4, e7 = p3 - p4, e8 = v4 - v3, e9 = p4 - p3;
+    float Lff15 = ((e6 * v3 + e7 * a3) + e8 * v4) + e9 * a4;
+    float LfD15 = fabsf(e7) * sig7 + fabsf(e9) * sig9;
+    float Lg13 = c7 * 50.0f, Lg15 = e7 * 50.0f;
+    const float gg = (float)(prm.gamma_b + prm.gamma_b);
+    const float g2 = (float)(prm.gamma_b * prm.gamma_b);
+    h[0] = (((Lff13 - LfD13) + gg * h13d) + g2 * h13) + Lg13 * u;
+    h[1] = (((Lff15 - LfD15) + gg * h15d) + g2 * h15) + Lg15 * u;
+    G[0][0] = -Lg13;
+    G[0][1] = -200.0f;
+    G[1][0] = -Lg15;
+    G[1][1] = -200.0f;
+    G[2][0] = 1.0f;
+    G[2][1] = 0.0f;
+    h[2] = (float)prm.u_max[0] - u;
+    G[3][0] = -1.0f;
+    G[3][1] = 0.0f;
+    h[3] = -(float)prm.u_min[0] + u;
+}
+
+// SimulatedCars, CascadeCBFLayer form (cbf_qp.py:149-219), fp64: no robust
+// term, mean/sigma ignored (:210-211).
+__device__ __forceinline__ void cars_rows_cascade(const rcbf_params& prm, const double* xs, double u,
+                                                  double (*G)[2], double* h) {
+#pragma clang fp contract(off)
+    const double kp = prm.kp, kb = prm.k_brake, g = prm.gamma_b;
+    double p0 = xs[0], p1 = xs[2], p2 = xs[4], p3 = xs[6], p4 = xs[8];
+    double v1 = xs[3], v2 = xs[5], v3 = xs[7], v4 = xs[9];
+    double a2 = kp * (30.0 - v2), a4 = kp * (30.0 - v4);
+    double d01 = p0 - p1, d12 = p1 - p2, d24 = p2 - p4;
+    (void)d01;
+    (void)v1;
+    a2 = a2 - kb * d12 * (d12 < 6.0 ? 1.0 : 0.0);
+    a4 = a4 - kb * d24 * (d24 < 13.0 ? 1.0 : 0.0);
+    const double a3 = 0.0;
+    double h13 = 0.5 * ((p2 - p3) * (p2 - p3) - 12.25);
+    double h15 = 0.5 * ((p4 - p3) * (p4 - p3) - 12.25);
+    double h13d = (p3 - p2) * (v3 - v2);
+    double h15d = (p3 - p4) * (v3 - v4);
+    double Lff13 = (((v2 - v3) * v2 + (p2 - p3) * a2) + (v3 - v2) * v3) + (p3 - p2) * a3;
+    double Lff15 = (((v3 - v4) * v3 + (p3 - p4) * a3) + (v4 - v3) * v4) + (p4 - p3) * a4;
+    double Lg13 = (p3 - p2) * 50.0, Lg15 = (p3 - p4) * 50.0;
+    h[0] = ((Lff13 + (g + g) * h13d) + g * g * h13) + Lg13 * u;
+    h[1] = ((Lff15 + (g + g) * h15d) + g * g * h15) + Lg15 * u;
+    G[0][0] = -Lg13;
+    G[0][1] = -2e2;
+    G[1][0] = -Lg15;
+    G[1][1] = -2e2;
+    G[2][0] = 1.0;
+    G[2][1] = 0.0;
+    h[2] = prm.u_max[0] - u;
+    G[3][0] = -1.0;
+    G[3][1] = 0.0;
+    h[3] = -prm.u_min[0] + u;
+}
+
+// Unicycle, CBFQPLayer form (diff_cbf_qp.py:202-266, actuators 362-377), fp32.
+// K hazards -> rows 0..K-1; actuator rows K..K+3 in the reference's order.
+template <int K>
+__device__ __forceinline__ void uni_rows_diff(const rcbf_params& prm, const float* xs, const float* u,
+                                              const float* mu, const float* sig, float (*G)[3],
+                                              float* h) {
+#pragma clang fp contract(off)
+    const float lp = (float)prm.l_p, g = (float)prm.gamma_b;
+    // fp32 cos/sin, correctly rounded from fp64 (torch's SLEEF is within 1 ulp)
+    float c = (float)cos((double)xs[2]);
+    float s = (float)sin((double)xs[2]);
+    float px = xs[0] + lp * c, py = xs[1] + lp * s;
+    float g00 = c, g01 = -s * lp, g10 = s, g11 = c * lp;
+    float mupx = g01 * mu[2] + mu[0], mupy = g11 * mu[2] + mu[1];
+    float sgpx = fabsf(g01) * sig[2] + sig[0], sgpy = fabsf(g11) * sig[2] + sig[1];
+    const float r2 = (float)((1.2 * prm.hazards_radius) * (1.2 * prm.hazards_radius));
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        float ox = (float)prm.hazards_xy[2 * j], oy = (float)prm.hazards_xy[2 * j + 1];
+        float dx = px - ox, dy = py - oy;
+        float hs = 0.5f * ((dx * dx + dy * dy) - r2);
+        float a0 = dx * g00 + dy * g10;
+        float a1 = dx * g01 + dy * g11;
+        float t1 = dx * mupx + dy * mupy;
+        float t2 = fabsf(dx) * sgpx + fabsf(dy) * sgpy;
+        float t3 = a0 * u[0] + a1 * u[1];
+        G[j][0] = -a0;
+        G[j][1] = -a1;
+        G[j][2] = -1.0f;
+        h[j] = g * ((hs * hs) * hs) + ((t1 - t2) + t3);
+    }
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2) {
+        const int r0 = K + 2 * c2;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            G[r0][k] = (k == c2) ? 1.0f : 0.0f;
+            G[r0 + 1][k] = (k == c2) ? -1.0f : 0.0f;
+        }
+        h[r0] = (float)prm.u_max[c2] - u[c2];
+        h[r0 + 1] = -(float)prm.u_min[c2] + u[c2];
+    }
+}
+
+// Unicycle, CascadeCBFLayer form (cbf_qp.py:91-147), fp64: signed sigma_p,
+// robust term x k_d.
+template <int K>
+__device__ __forceinline__ void uni_rows_cascade(const rcbf_params& prm, const double* xs, const double* u,
+                                                 const double* mu, const double* sig, double (*G)[3],
+                                                 double* h) {
+#pragma clang fp contract(off)
+    const double lp = prm.l_p, g = prm.gamma_b, kd = prm.k_d;
+    double c = cos(xs[2]), s = sin(xs[2]);
+    double px = xs[0] + lp * c, py = xs[1] + lp * s;
+    double g00 = c, g01 = -s * lp, g10 = s, g11 = c * lp;
+    double mpx = mu[0] + lp * (-s) * mu[2], mpy = mu[1] + lp * c * mu[2];
+    double spx = sig[0] + lp * (-s) * sig[2], spy = sig[1] + lp * c * sig[2];
+    const double r2 = (1.2 * prm.hazards_radius) * (1.2 * prm.hazards_radius);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double dx = px - prm.hazards_xy[2 * j], dy = py - prm.hazards_xy[2 * j + 1];
+        double hs = 0.5 * ((dx * dx + dy * dy) - r2);
+        double a0 = dx * g00 + dy * g10, a1 = dx * g01 + dy * g11;
+        G[j][0] = -a0;
+        G[j][1] = -a1;
+        G[j][2] = -1.0;
+        h[j] = ((g * (hs * hs * hs) + (dx * mpx + dy * mpy)) + (a0 * u[0] + a1 * u[1])) -
+               kd * (fabs(dx) * spx + fabs(dy) * spy);
+    }
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2) {
+        const int r0 = K + 2 * c2;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            G[r0][k] = (k == c2) ? 1.0 : 0.0;
+            G[r0 + 1][k] = (k == c2) ? -1.0 : 0.0;
+        }
+        h[r0] = prm.u_max[c2] - u[c2];
+        h[r0 + 1] = -prm.u_min[c2] + u[c2];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// environments (fp64, numpy order, no contraction)
+// ---------------------------------------------------------------------------
+struct CarsStepOut {
+    float reward;
+    double reward_d;
+    double cost;
+    bool done;
+};
+
+// SimulatedCarsEnv.step (simulated_cars_env.py:38-106): true dynamics with
+// the lead car's sin term, car 4's kp drift kept, x1.1 on every acceleration.
+template <typename A>
+__device__ __forceinline__ void cars_env_step(const rcbf_params& prm, double* xs, double& t, int& step, A action,
+                                              CarsStepOut& o) {
+#pragma clang fp contract(off)
+    const double kp = prm.kp, kb = prm.k_brake, dt = 0.02;
+    double vdes0 = 30.0 - 10.0 * sin(0.2 * t);
+    double acc[5];
+    acc[0] = kp * (vdes0 - xs[1]);
+#pragma unroll
+    for (int i = 1; i < 5; ++i) acc[i] = kp * (30.0 - xs[2 * i + 1]);
+    double d01 = xs[0] - xs[2], d12 = xs[2] - xs[4], d24 = xs[4] - xs[8];
+    acc[1] += (-kb * d01) * (d01 < 6.0 ? 1.0 : 0.0);
+    acc[2] += (-kb * d12) * (d12 < 6.0 ? 1.0 : 0.0);
+    acc[4] += (-kb * d24) * (d24 < 13.0 ? 1.0 : 0.0);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) acc[i] *= 1.1;
+    const double gu = 50.0 * (double)action;
+    double v[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) v[i] = xs[2 * i + 1];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        xs[2 * i] += dt * (v[i] + 0.0);
+        xs[2 * i + 1] += dt * (acc[i] + (i == 3 ? gu : 0.0));
+    }
+    t = t + dt;
+    step += 1;
+    o.done = step >= 300;
+    // reward in the action's dtype (-5.0 * abs(a**2) / 300), :93
+    A a2 = action * action;
+    A r = (A)(-5.0) * (a2 < (A)0 ? -a2 : a2) / (A)300;
+    o.reward = (float)r;
+    o.reward_d = (double)r;
+    double cost = 0.0;
+    if (xs[4] - xs[6] < 2.99) cost -= 0.1;
+    if (xs[6] - xs[8] < 2.99) cost -= 0.1;
+    o.cost = cost;
+}
+
+__device__ __forceinline__ void cars_obs(const double* xs, double* o) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        o[2 * i] = xs[2 * i] / 100.0;
+        o[2 * i + 1] = xs[2 * i + 1] / 30.0;
+    }
+}
+
+__device__ __forceinline__ double uni_goal_dist(const double* xs) {
+#pragma clang fp contract(off)
+    double d0 = 2.5 - xs[0], d1 = 2.5 - xs[1];
+    return sqrt(d0 * d0 + d1 * d1);
+}
+
+// UnicycleEnv.get_obs (unicycle_env.py:215-231) + obs_compass (:260-277)
+__device__ __forceinline__ void uni_obs(const double* xs, double* o) {
+#pragma clang fp contract(off)
+    double r0 = 2.5 - xs[0], r1 = 2.5 - xs[1];
+    double gd = sqrt(r0 * r0 + r1 * r1);
+    double c = cos(xs[2]), s = sin(xs[2]);
+    double v0 = r0 * c + r1 * s;
+    double v1 = r0 * (-s) + r1 * c;
+    double nrm = sqrt(v0 * v0 + v1 * v1) + 0.001;
+    o[0] = xs[0];
+    o[1] = xs[1];
+    o[2] = c;
+    o[3] = s;
+    o[4] = v0 / nrm;
+    o[5] = v1 / nrm;
+    o[6] = exp(-gd);
+}
+
+struct UniStepOut {
+    double reward;
+    double cost;
+    bool done;
+    bool goal;
+};
+
+// UnicycleEnv.step/_step (unicycle_env.py:46-111): clip to +-1 after the
+// safety filter, Euler step with g(x), then the -(dt*0.1) g(x') [cos th', 0]
+// drift evaluated left to right (:87).
+template <typename A>
+__device__ __forceinline__ void uni_env_step(const rcbf_params& prm, double* xs, double& last_dist, int& step,
+                                             const A* action, UniStepOut& o) {
+#pragma clang fp contract(off)
+    A a0c = action[0] < (A)(-1) ? (A)(-1) : (action[0] > (A)1 ? (A)1 : action[0]);
+    A a1c = action[1] < (A)(-1) ? (A)(-1) : (action[1] > (A)1 ? (A)1 : action[1]);
+    double a0 = (double)a0c, a1 = (double)a1c;
+    const double dt = 0.02;
+    double c = cos(xs[2]), s = sin(xs[2]);
+    xs[0] += dt * (0.0 + c * a0);
+    xs[1] += dt * (0.0 + s * a0);
+    xs[2] += dt * (0.0 + a1);
+    double c2 = cos(xs[2]), s2 = sin(xs[2]);
+    const double k = dt * 0.1;
+    xs[0] -= (k * c2) * c2;
+    xs[1] -= (k * s2) * c2;
+    step += 1;
+    double d = uni_goal_dist(xs);
+    double reward = last_dist - d;
+    last_dist = d;
+    bool goal = d <= 0.3;
+    if (goal) reward += 1.0;
+    o.goal = goal;
+    o.done = goal || (step >= 1000);
+    o.reward = reward;
+    bool hit = false;
+    const double r2 = prm.hazards_radius * prm.hazards_radius;
+    for (int j = 0; j < prm.num_hazards; ++j) {
+        double ex = xs[0] - prm.hazards_xy[2 * j], ey = xs[1] - prm.hazards_xy[2 * j + 1];
+        hit = hit || (ex * ex + ey * ey < r2);
+    }
+    o.cost = hit ? 0.1 : 0.0;
+}
+
+// ---------------------------------------------------------------------------
+// counter-based RNG (Philox4x32-10) for the cars reset draw N(0, 0.5)
+// keyed by (seed, global env index, episode counter) -> independent of how
+// envs are sharded over GPUs.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+        uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+        uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+__device__ __forceinline__ double normal_draw(uint64_t seed, uint64_t env, uint32_t episode) {
+    uint32_t c[4] = {(uint32_t)env, (uint32_t)(env >> 32), episode, 0x5AFEu};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    // two 53-bit uniforms in (0,1] -> Box-Muller
+    uint64_t a = ((uint64_t)c[0] << 21) ^ (uint64_t)c[1];
+    uint64_t b = ((uint64_t)c[2] << 21) ^ (uint64_t)c[3];
+    double u1 = ((double)(a & ((1ull << 53) - 1)) + 1.0) * (1.0 / 9007199254740992.0);
+    double u2 = (double)(b & ((1ull << 53) - 1)) * (1.0 / 9007199254740992.0);
+    return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+__device__ __forceinline__ void cars_reset_state(double* xs, double noise) {
+    const double p0[5] = {34.0, 28.0, 22.0, 16.0, 10.0};
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        xs[2 * i] = p0[i];
+        xs[2 * i + 1] = 30.0 + noise;
+    }
+    xs[7] = 35.0;
+}
+
+__device__ __forceinline__ void uni_reset_state(double* xs, double& last_dist) {
+    xs[0] = -2.5;
+    xs[1] = -2.5;
+    xs[2] = 0.0;
+    last_dist = uni_goal_dist(xs);
+}
+
+}  // namespace rcbf

@@ -1,0 +1,122 @@
+"""ctypes binding of librcbf_hip.so (C-ABI declared in include/rcbf_hip.h).
+
+The product path is HIP only: if the shared library is missing or fails to
+load, every entry point raises -- there is no CPU or PyTorch fallback.
+torch is imported first so the process has exactly one HIP runtime
+(torch's libamdhip64.so.7; ours binds to the same soname).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime the library binds to)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RCBF_HIP_LIB", os.path.join(_HERE, "librcbf_hip.so"))
+
+MODE_SIMULATED_CARS = 0
+MODE_UNICYCLE = 1
+FORM_DIFF = 0
+FORM_CASCADE = 1
+SOLVER_ACTIVE_SET = 0
+SOLVER_PDIPM = 1
+QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NONFINITE = 0, 1, 2, 3
+MAX_HAZARDS = 8
+ABI_VERSION = 2
+
+_ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL"}
+
+
+class RcbfParams(ctypes.Structure):
+    """Mirror of `rcbf_params` (include/rcbf_hip.h)."""
+    _fields_ = [
+        ("mode", ctypes.c_int32),
+        ("formulation", ctypes.c_int32),
+        ("num_hazards", ctypes.c_int32),
+        ("solver", ctypes.c_int32),
+        ("max_iter", ctypes.c_int32),
+        ("_pad", ctypes.c_int32),
+        ("gamma_b", ctypes.c_double),
+        ("k_d", ctypes.c_double),
+        ("l_p", ctypes.c_double),
+        ("kp", ctypes.c_double),
+        ("k_brake", ctypes.c_double),
+        ("u_min", ctypes.c_double * 2),
+        ("u_max", ctypes.c_double * 2),
+        ("hazards_radius", ctypes.c_double),
+        ("hazards_xy", ctypes.c_double * (2 * MAX_HAZARDS)),
+        ("eps", ctypes.c_double),
+    ]
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_U64 = ctypes.c_uint64
+_PRM = ctypes.POINTER(RcbfParams)
+
+SIGNATURES = {
+    "rcbf_build": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_build_f64": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_qp_solve": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P],
+    "rcbf_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_cascade_u_safe": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_env_reset": [_PRM, _I64, _P, _P, _U64, _I64, _P, _P, _P, _P, _P, _P],
+    "rcbf_env_step": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
+    "rcbf_safe_step": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
+    "rcbf_safe_rollout": [_PRM, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _P],
+    "rcbf_version": [],
+    "rcbf_abi_version": [],
+    "rcbf_params_size": [],
+}
+
+_lib = None
+_load_error = None
+
+
+def load():
+    """Load the library once; raise (never fall back) if it is unavailable."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise _load_error
+    if not os.path.exists(LIB_PATH):
+        _load_error = RuntimeError(
+            f"librcbf_hip.so not found at {LIB_PATH}: build it with `python __graft_entry__.py build` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        raise _load_error
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int32
+    lib.rcbf_version.restype = ctypes.c_char_p
+    if lib.rcbf_abi_version() != ABI_VERSION or lib.rcbf_params_size() != ctypes.sizeof(RcbfParams):
+        raise RuntimeError("librcbf_hip.so ABI mismatch (rebuild with `python __graft_entry__.py build`)")
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = _ERRORS.get(rc, f"hipError_t {rc}")
+        raise RuntimeError(f"{what} failed: {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(t, name):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a HIP device tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")

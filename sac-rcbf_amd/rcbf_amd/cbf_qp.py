@@ -1,0 +1,90 @@
+"""Drop-in `CascadeCBFLayer` (rcbf_sac/cbf_qp.py:5-358) on the HIP kernels.
+
+get_u_safe builds the fp64 rows, normalises them and solves the QP exactly
+(Goldfarb-Idnani, the algorithm of the quadprog call at cbf_qp.py:276) in one
+launch of rcbf_cascade_u_safe.  It also accepts a batch (leading axis).
+The reference's per-call print of the quadprog result (:278) is not kept.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .dynamics import DYNAMICS_MODE
+from .params import make_params
+
+
+class CascadeCBFLayer:
+
+    def __init__(self, env, gamma_b=100, k_d=1.5, l_p=0.03, solver=_lib.SOLVER_ACTIVE_SET):
+        self.env = env
+        self.u_min, self.u_max = self.get_control_bounds()
+        self.gamma_b = gamma_b
+        self.k_d = k_d
+        self.l_p = l_p
+        if self.env.dynamics_mode not in DYNAMICS_MODE:
+            raise Exception("Dynamics mode not supported.")
+        self._prm = make_params(env, gamma_b, k_d, l_p, _lib.FORM_CASCADE, solver)
+        _lib.load()
+
+    def get_u_safe(self, u_nom, s, mean_pred, sigma):
+        """cbf_qp.py:29-53: u_safe such that env.step(u_nom + u_safe) is safe."""
+        if not torch.cuda.is_available():
+            raise RuntimeError("CascadeCBFLayer needs a HIP device (MI355X); there is no CPU fallback")
+        un = np.asarray(u_nom, np.float64)
+        single = un.ndim == 1
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+        def d(a):
+            return torch.as_tensor(np.atleast_2d(np.asarray(a, np.float64)), device=dev).contiguous()
+
+        U, X, M, S = d(un), d(s), d(mean_pred), d(sigma)
+        B = X.shape[0]
+        out = torch.empty(B, U.shape[1], dtype=torch.float64, device=dev)
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        rc = _lib.load().rcbf_cascade_u_safe(ctypes.byref(self._prm), B, _lib.ptr(U), _lib.ptr(X), _lib.ptr(M),
+                                             _lib.ptr(S), _lib.ptr(out), None, _lib.ptr(flag), _lib.stream_of(dev))
+        _lib.check(rc, "rcbf_cascade_u_safe")
+        if int(flag.item()):
+            raise ValueError("constraints are inconsistent, no solution")  # quadprog's ValueError (:279-281)
+        res = out.cpu().numpy()
+        return res[0] if single else res
+
+    def get_cbf_qp_constraints(self, u_nom, state, mean_pred, sigma_pred):
+        """cbf_qp.py:55-240 (fp64), single sample or batch."""
+        un = np.asarray(u_nom, np.float64)
+        single = un.ndim == 1
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+        def d(a):
+            return torch.as_tensor(np.atleast_2d(np.asarray(a, np.float64)), device=dev).contiguous()
+
+        U, X, M, S = d(un), d(state), d(mean_pred), d(sigma_pred)
+        B = X.shape[0]
+        n = U.shape[1] + 1
+        m = (len(self.env.hazards_locations) if self.env.dynamics_mode == "Unicycle" else 2) + 2 * U.shape[1]
+        P = torch.empty(B, n, n, dtype=torch.float64, device=dev)
+        q = torch.empty(B, n, dtype=torch.float64, device=dev)
+        G = torch.empty(B, m, n, dtype=torch.float64, device=dev)
+        h = torch.empty(B, m, dtype=torch.float64, device=dev)
+        rc = _lib.load().rcbf_build_f64(ctypes.byref(self._prm), B, _lib.ptr(X), _lib.ptr(U), _lib.ptr(M),
+                                        _lib.ptr(S), _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h),
+                                        _lib.stream_of(dev))
+        _lib.check(rc, "rcbf_build_f64")
+        P, q, G, h = (t.cpu().numpy() for t in (P, q, G, h))
+        if single:
+            return P[0], q[0], G[0], h[0]
+        return P, q, G, h
+
+    def get_control_bounds(self):
+        return self.env.safe_action_space.low, self.env.safe_action_space.high
+
+    def get_min_h_val(self, state):
+        """cbf_qp.py:341-358 (uses the r + 0.07 radius of get_cbfs :308)."""
+        hz = np.asarray(self.env.hazards_locations)
+        r = self.env.hazards_radius + 0.07
+        st = np.asarray(state, np.float64)
+        if self.env.dynamics_mode == "Unicycle":
+            st = np.array([st[0] + self.l_p * np.cos(st[2]), st[1] + self.l_p * np.sin(st[2])])
+        return np.min(0.5 * (np.sum((st - hz) ** 2, axis=1) - r ** 2))

@@ -1,0 +1,186 @@
+"""Drop-in `CBFQPLayer` (rcbf_sac/diff_cbf_qp.py:10-395) on the HIP kernels.
+
+Same constructor, attributes, methods and exceptions as the reference; the
+whole get_safe_action (build -> row normalise -> fp64 QP -> clamp) is ONE
+kernel launch (rcbf_safe_action) and its backward w.r.t. the action is one
+more (rcbf_safe_action_backward).  No qpth, no CPU path: inputs on the CPU are
+moved to the HIP device for the launch and the result is moved back.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .dynamics import DYNAMICS_MODE
+from .params import make_params
+
+_QP_FAILED = "QP Failed to solve"
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        raise RuntimeError("CBFQPLayer needs a HIP device (MI355X); there is no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _f32(t, dev):
+    if not torch.is_tensor(t):
+        t = torch.as_tensor(np.asarray(t))
+    return t.detach().to(device=dev, dtype=torch.float32).contiguous()
+
+
+def _raise_if_failed(flag):
+    bits = int(flag.item())  # one 4-byte read (the reference syncs here too, :141)
+    if bits:
+        raise Exception(_QP_FAILED)
+
+
+class _SafeAction(torch.autograd.Function):
+    """final = clamp(u + QP(u)[:n_u]);  grad flows to `u` only, like the
+    reference whose state/mean/sigma arrive detached (dynamics.py:211,362)."""
+
+    @staticmethod
+    def forward(ctx, layer, x, u, mu, sigma):
+        lib = _lib.load()
+        B = x.shape[0]
+        out = torch.empty_like(u)
+        flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+        rc = lib.rcbf_safe_action(ctypes.byref(layer._prm), B, _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu),
+                                  _lib.ptr(sigma), _lib.ptr(out), None, _lib.ptr(flag),
+                                  _lib.stream_of(x.device))
+        _lib.check(rc, "rcbf_safe_action")
+        if layer.check_failures:
+            _raise_if_failed(flag)
+        ctx.layer = layer
+        ctx.save_for_backward(x, u, mu, sigma)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        x, u, mu, sigma = ctx.saved_tensors
+        lib = _lib.load()
+        g = grad.contiguous().to(torch.float32)
+        gu = torch.empty_like(u)
+        rc = lib.rcbf_safe_action_backward(ctypes.byref(ctx.layer._prm), x.shape[0], _lib.ptr(x), _lib.ptr(u),
+                                           _lib.ptr(mu), _lib.ptr(sigma), _lib.ptr(g), _lib.ptr(gu),
+                                           _lib.stream_of(x.device))
+        _lib.check(rc, "rcbf_safe_action_backward")
+        return None, None, gu, None, None
+
+
+class CBFQPLayer:
+
+    def __init__(self, env, args, gamma_b=100, k_d=1.5, l_p=0.03, solver=_lib.SOLVER_ACTIVE_SET):
+        """rcbf_sac/diff_cbf_qp.py:12-42 (same arguments and attributes).
+        `solver` selects the fp64 QP algorithm: exact Goldfarb-Idnani active
+        set (default) or the qpth-style primal-dual interior point."""
+        self.device = torch.device("cuda" if getattr(args, "cuda", False) else "cpu")
+        self.env = env
+        self.u_min, self.u_max = self.get_control_bounds()
+        self.gamma_b = gamma_b
+        if self.env.dynamics_mode not in DYNAMICS_MODE:
+            raise Exception("Dynamics mode not supported.")
+        if self.env.dynamics_mode == "Unicycle":
+            self.num_cbfs = len(env.hazards_locations)
+            self.k_d = k_d
+            self.l_p = l_p
+        elif self.env.dynamics_mode == "SimulatedCars":
+            self.num_cbfs = 2
+        self.action_dim = env.action_space.shape[0]
+        self.num_ineq_constraints = self.num_cbfs + 2 * self.action_dim
+        self._prm = make_params(env, gamma_b, k_d, l_p, _lib.FORM_DIFF, solver)
+        self.check_failures = True
+        _lib.load()
+
+    # -- diff_cbf_qp.py:44-79 ----------------------------------------------
+    def get_safe_action(self, state_batch, action_batch, mean_pred_batch, sigma_pred_batch):
+        expand_dims = len(state_batch.shape) == 1
+        if expand_dims:
+            action_batch = action_batch.unsqueeze(0)
+            state_batch = state_batch.unsqueeze(0)
+            mean_pred_batch = mean_pred_batch.unsqueeze(0) if mean_pred_batch is not None else None
+            sigma_pred_batch = sigma_pred_batch.unsqueeze(0) if sigma_pred_batch is not None else None
+        out_device = action_batch.device if torch.is_tensor(action_batch) else self.device
+        dev = _dev()
+        x = _f32(state_batch, dev)
+        mu = _f32(mean_pred_batch, dev) if mean_pred_batch is not None else None
+        sig = _f32(sigma_pred_batch, dev) if sigma_pred_batch is not None else None
+        if torch.is_tensor(action_batch) and action_batch.requires_grad:
+            u = action_batch.to(device=dev, dtype=torch.float32)
+            if not u.is_contiguous():
+                u = u.contiguous()
+        else:
+            u = _f32(action_batch, dev)
+        self._check_shapes(x, u, mu, sig)
+        final_action = _SafeAction.apply(self, x, u, mu, sig)
+        if final_action.device != out_device:
+            final_action = final_action.to(out_device)
+        return final_action if not expand_dims else final_action.squeeze(0)
+
+    def _check_shapes(self, x, u, mu, sig):
+        n_s = DYNAMICS_MODE[self.env.dynamics_mode]["n_s"]
+        B = x.shape[0]
+        if x.dim() != 2 or x.shape[1] != n_s or u.shape != (B, self.action_dim):
+            raise ValueError(f"expected state (B,{n_s}) and action (B,{self.action_dim}), got "
+                             f"{tuple(x.shape)} / {tuple(u.shape)}")
+        for t in (mu, sig):
+            if t is not None and t.shape != x.shape:
+                raise ValueError("mean/sigma must have the state's shape")
+
+    # -- diff_cbf_qp.py:146-379 --------------------------------------------
+    def get_cbf_qp_constraints(self, state_batch, action_batch, mean_pred_batch, sigma_pred_batch):
+        assert len(state_batch.shape) == 2 and len(action_batch.shape) == 2 and len(mean_pred_batch.shape) == 2 \
+            and len(sigma_pred_batch.shape) == 2, (state_batch.shape, action_batch.shape)
+        dev = _dev()
+        x, u = _f32(state_batch, dev), _f32(action_batch, dev)
+        mu, sig = _f32(mean_pred_batch, dev), _f32(sigma_pred_batch, dev)
+        self._check_shapes(x, u, mu, sig)
+        B, n, m = x.shape[0], self.action_dim + 1, self.num_ineq_constraints
+        P = torch.empty(B, n, n, device=dev)
+        q = torch.empty(B, n, device=dev)
+        G = torch.empty(B, m, n, device=dev)
+        h = torch.empty(B, m, device=dev)
+        rc = _lib.load().rcbf_build(ctypes.byref(self._prm), B, _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu),
+                                    _lib.ptr(sig), _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h),
+                                    _lib.stream_of(dev))
+        _lib.check(rc, "rcbf_build")
+        od = state_batch.device if torch.is_tensor(state_batch) else self.device
+        return P.to(od), q.to(od), G.to(od), h.to(od)
+
+    # -- diff_cbf_qp.py:81-109 ---------------------------------------------
+    def solve_qp(self, Ps, qs, Gs, hs):
+        """Row-normalise then solve; returns the solution without the slack."""
+        sol = self._qp(Ps, qs, Gs, hs, normalize=True)
+        return sol[:, :-1]
+
+    # -- diff_cbf_qp.py:111-144 --------------------------------------------
+    def cbf_layer(self, Qs, ps, Gs, hs, As=None, bs=None, solver_args=None):
+        if As is not None and As.numel() > 0:
+            raise NotImplementedError("equality constraints are not used on this path (diff_cbf_qp.py:135-137)")
+        return self._qp(Qs, ps, Gs, hs, normalize=False)
+
+    def _qp(self, Ps, qs, Gs, hs, normalize):
+        if any(t.requires_grad for t in (Ps, qs, Gs, hs) if torch.is_tensor(t)):
+            raise NotImplementedError(
+                "gradients through cbf_layer/solve_qp directly are not provided; use get_safe_action, whose "
+                "backward covers the QP, the row normaliser and the clamp")
+        dev = _dev()
+        P, G, h = _f32(Ps, dev), _f32(Gs, dev), _f32(hs, dev)
+        q = _f32(qs, dev) if qs is not None else None
+        B, m, n = G.shape
+        z = torch.empty(B, n, device=dev)
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        rc = _lib.load().rcbf_qp_solve(ctypes.byref(self._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G),
+                                       _lib.ptr(h), int(normalize), _lib.ptr(z), None, None, _lib.ptr(flag),
+                                       _lib.stream_of(dev))
+        _lib.check(rc, "rcbf_qp_solve")
+        _raise_if_failed(flag)
+        od = Gs.device if torch.is_tensor(Gs) else self.device
+        return z.to(od)
+
+    # -- diff_cbf_qp.py:381-395 --------------------------------------------
+    def get_control_bounds(self):
+        u_min = torch.tensor(self.env.safe_action_space.low).to(self.device)
+        u_max = torch.tensor(self.env.safe_action_space.high).to(self.device)
+        return u_min, u_max

@@ -1,0 +1,349 @@
+"""Device-resident environments (envs/simulated_cars_env.py, envs/unicycle_env.py).
+
+* BatchedSimulatedCarsEnv / BatchedUnicycleEnv: B envs whose fp64 state lives
+  in HBM; reset/step/safe_step/rollout are single HIP launches (rcbf_env_*,
+  rcbf_safe_step, rcbf_safe_rollout) with auto-reset of finished envs.
+* SimulatedCarsEnv / UnicycleEnv: the reference's single-env gym API
+  (reset() -> obs, step(a) -> (obs, reward, done, info), seed/close/render,
+  action_space/observation_space/safe_action_space, max_episode_steps, dt,
+  dynamics_mode, kp/k_brake, hazards_*) on a B = 1 device env, so the
+  reference's main.py loop runs unchanged.
+
+Per-env state: x (B, n_s) f64 = env.state; aux (B,) f64 = env.t (cars) or
+env.last_goal_dist (unicycle); step (B,) i32 = env.episode_step; episode
+(B,) i32 = reset counter keying the counter-based reset RNG (so the cars'
+N(0, 0.5) reset draw depends only on (seed, global env index, episode) and is
+identical however the envs are sharded over GPUs).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .params import make_params
+
+try:  # keep gym's types when gym is installed (it is not in this image)
+    import gym as _gym
+    _EnvBase = _gym.Env
+except Exception:  # pragma: no cover - exercised when gym is absent
+    _gym = None
+    _EnvBase = object
+
+
+class Box:
+    """Minimal gym.spaces.Box: float32 low/high/shape, sample/seed/contains."""
+
+    def __init__(self, low, high, shape):
+        self.shape = tuple(shape)
+        self.low = np.full(self.shape, low, dtype=np.float32)
+        self.high = np.full(self.shape, high, dtype=np.float32)
+        self.dtype = np.float32
+        self._rng = np.random.RandomState()
+
+    def seed(self, s=None):
+        self._rng = np.random.RandomState(s)
+        return [s]
+
+    def sample(self):
+        return self._rng.uniform(self.low, self.high).astype(np.float32)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low)) and bool(np.all(x <= self.high))
+
+
+def _box(low, high, shape):
+    if _gym is not None:
+        return _gym.spaces.Box(low=low, high=high, shape=shape)
+    return Box(low, high, shape)
+
+
+class _EnvSpec:
+    """Constants of one env family (the reference's __init__ attributes)."""
+
+    def __init__(self, mode):
+        self.dynamics_mode = mode
+        if mode == "SimulatedCars":  # simulated_cars_env.py:17-26
+            self.action_space = _box(-1.0, 1.0, (1,))
+            self.safe_action_space = _box(-10.0, 10.0, (1,))
+            self.observation_space = _box(-1e10, 1e10, (10,))
+            self.max_episode_steps = 300
+            self.dt = 0.02
+            self.kp = 4.0
+            self.k_brake = 20.0
+            self.n_s, self.n_u, self.n_o = 10, 1, 10
+        else:  # unicycle_env.py:17-34
+            self.action_space = _box(-1.0, 1.0, (2,))
+            self.safe_action_space = _box(-2.5, 2.5, (2,))
+            self.observation_space = _box(-1e10, 1e10, (7,))
+            self.bds = np.array([[-3., -3.], [3., 3.]])
+            self.hazards_radius = 0.6
+            self.hazards_locations = np.array([[0., 0.], [-1., 1.], [-1., -1.], [1., -1.], [1., 1.]]) * 1.5
+            self.dt = 0.02
+            self.max_episode_steps = 1000
+            self.reward_goal = 1.0
+            self.goal_size = 0.3
+            self.goal_pos = np.array([2.5, 2.5])
+            self.n_s, self.n_u, self.n_o = 3, 2, 7
+
+
+class BatchedEnv:
+    """B independent envs resident on one HIP device."""
+
+    def __init__(self, mode, num_envs, device=None, seed=0, env_offset=0, hazards_locations=None):
+        spec = _EnvSpec(mode)
+        self.__dict__.update({k: v for k, v in spec.__dict__.items()})
+        if hazards_locations is not None:
+            self.hazards_locations = np.asarray(hazards_locations, np.float64).reshape(-1, 2)
+        if not torch.cuda.is_available():
+            raise RuntimeError("device envs need a HIP device (MI355X); there is no CPU fallback")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.num_envs = int(num_envs)
+        self.seed_value = int(seed)
+        self.env_offset = int(env_offset)  # global index of env 0 (sharding)
+        B, d = self.num_envs, self.device
+        self.x = torch.zeros(B, self.n_s, dtype=torch.float64, device=d)
+        self.aux = torch.zeros(B, dtype=torch.float64, device=d)
+        self.step_count = torch.zeros(B, dtype=torch.int32, device=d)
+        self.episode = torch.zeros(B, dtype=torch.int32, device=d)
+        self.obs = torch.zeros(B, self.n_o, dtype=torch.float32, device=d)
+        self._prm_env = make_params(self, 1.0)
+        self.fail_flag = torch.zeros(1, dtype=torch.int32, device=d)
+        _lib.load()
+        self.reset()
+
+    def _rng_seed(self):
+        return self.seed_value & 0xFFFFFFFFFFFFFFFF
+
+    def _stream(self):
+        return _lib.stream_of(self.device)
+
+    def reset(self, noise=None, mask=None):
+        """Reset all envs (or those with mask != 0).  `noise` (B,) f64 injects
+        the cars' N(0,0.5) velocity draw (simulated_cars_env.py:120)."""
+        nz = None
+        if noise is not None:
+            nz = torch.as_tensor(noise, dtype=torch.float64, device=self.device).reshape(-1).contiguous()
+        mk = None
+        if mask is not None:
+            mk = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        rc = _lib.load().rcbf_env_reset(ctypes.byref(self._prm_env), self.num_envs, _lib.ptr(mk), _lib.ptr(nz),
+                                        self._rng_seed(), self.env_offset, _lib.ptr(self.x), _lib.ptr(self.aux),
+                                        _lib.ptr(self.step_count), _lib.ptr(self.episode), _lib.ptr(self.obs),
+                                        self._stream())
+        _lib.check(rc, "rcbf_env_reset")
+        return self.obs
+
+    def step(self, action, auto_reset=True, obs64=False):
+        """Batched env.step: action (B, n_u) f32 or f64 (reward dtype follows
+        the action like the reference).  Returns obs (B,n_o) f32, reward (B,)
+        f64, done (B,) bool, info dict(cost (B,) f64, goal_met (B,) bool[, obs64])."""
+        a = torch.as_tensor(action, device=self.device)
+        if a.dtype not in (torch.float32, torch.float64):
+            a = a.to(torch.float32)
+        a = a.reshape(self.num_envs, self.n_u).contiguous()
+        B, d = self.num_envs, self.device
+        reward = torch.empty(B, dtype=torch.float64, device=d)
+        cost = torch.empty(B, dtype=torch.float64, device=d)
+        done = torch.empty(B, dtype=torch.uint8, device=d)
+        goal = torch.empty(B, dtype=torch.uint8, device=d)
+        o64 = torch.empty(B, self.n_o, dtype=torch.float64, device=d) if obs64 else None
+        rc = _lib.load().rcbf_env_step(ctypes.byref(self._prm_env), B, _lib.ptr(self.x), _lib.ptr(self.aux),
+                                       _lib.ptr(self.step_count), _lib.ptr(self.episode), _lib.ptr(a),
+                                       int(a.dtype == torch.float64), _lib.ptr(o64), _lib.ptr(self.obs),
+                                       _lib.ptr(reward), _lib.ptr(cost), _lib.ptr(done), _lib.ptr(goal),
+                                       int(auto_reset), self._rng_seed(), self.env_offset, self._stream())
+        _lib.check(rc, "rcbf_env_step")
+        info = {"cost": cost, "goal_met": goal.bool()}
+        if obs64:
+            info["obs64"] = o64
+        return self.obs, reward, done.bool(), info
+
+    def safe_step(self, u_rl, layer, mean=None, sigma=None, auto_reset=True, outputs=None):
+        """The fused hot path (rcbf_safe_step): state -> get_state(obs32) ->
+        CBFQPLayer.get_safe_action(state, u_rl, mean, sigma) -> env.step.
+        mean/sigma None -> the DynamicsModel prior in-kernel.  `outputs`
+        (from make_outputs) avoids per-call allocation; failures accumulate
+        in self.fail_flag (check with check_failures())."""
+        B, d = self.num_envs, self.device
+        o = outputs if outputs is not None else self.make_outputs()
+        u = u_rl if (torch.is_tensor(u_rl) and u_rl.dtype == torch.float32 and u_rl.is_contiguous()
+                     and u_rl.device == d) else torch.as_tensor(u_rl, dtype=torch.float32, device=d).contiguous()
+        rc = _lib.load().rcbf_safe_step(ctypes.byref(layer._prm), B, _lib.ptr(self.x), _lib.ptr(self.aux),
+                                        _lib.ptr(self.step_count), _lib.ptr(self.episode), _lib.ptr(u),
+                                        _lib.ptr(mean), _lib.ptr(sigma), _lib.ptr(self.obs), _lib.ptr(o["u"]),
+                                        _lib.ptr(o["reward"]), _lib.ptr(o["cost"]), _lib.ptr(o["done"]),
+                                        _lib.ptr(o["goal_met"]), None, _lib.ptr(self.fail_flag), int(auto_reset),
+                                        self._rng_seed(), self.env_offset, self._stream())
+        _lib.check(rc, "rcbf_safe_step")
+        return self.obs, o["reward"], o["done"], o
+
+    def make_outputs(self):
+        B, d = self.num_envs, self.device
+        return {"u": torch.empty(B, self.n_u, dtype=torch.float32, device=d),
+                "reward": torch.empty(B, dtype=torch.float32, device=d),
+                "cost": torch.empty(B, dtype=torch.float32, device=d),
+                "done": torch.empty(B, dtype=torch.uint8, device=d),
+                "goal_met": torch.empty(B, dtype=torch.uint8, device=d)}
+
+    def rollout(self, u_rl_seq, layer):
+        """K fused safe steps in one launch (rcbf_safe_rollout) from a
+        pre-sampled u_rl (K, B, n_u) f32, prior mean/sigma, auto-reset.
+        Returns per-env reward sum, cost sum and episodes finished."""
+        B, d = self.num_envs, self.device
+        u = torch.as_tensor(u_rl_seq, dtype=torch.float32, device=d).contiguous()
+        K = u.shape[0]
+        rs = torch.empty(B, dtype=torch.float32, device=d)
+        cs = torch.empty(B, dtype=torch.float32, device=d)
+        nd = torch.empty(B, dtype=torch.int32, device=d)
+        rc = _lib.load().rcbf_safe_rollout(ctypes.byref(layer._prm), B, K, _lib.ptr(self.x), _lib.ptr(self.aux),
+                                           _lib.ptr(self.step_count), _lib.ptr(self.episode), _lib.ptr(u),
+                                           _lib.ptr(self.obs), _lib.ptr(rs), _lib.ptr(cs), _lib.ptr(nd),
+                                           _lib.ptr(self.fail_flag), self._rng_seed(), self.env_offset, self._stream())
+        _lib.check(rc, "rcbf_safe_rollout")
+        return rs, cs, nd
+
+    def check_failures(self):
+        bits = int(self.fail_flag.item())
+        if bits:
+            self.fail_flag.zero_()
+            raise Exception("QP Failed to solve")
+
+
+class BatchedSimulatedCarsEnv(BatchedEnv):
+    def __init__(self, num_envs, device=None, seed=0, env_offset=0):
+        super().__init__("SimulatedCars", num_envs, device, seed, env_offset)
+
+
+class BatchedUnicycleEnv(BatchedEnv):
+    def __init__(self, num_envs, device=None, seed=0, env_offset=0, hazards_locations=None):
+        super().__init__("Unicycle", num_envs, device, seed, env_offset, hazards_locations)
+
+
+class _SingleEnv(_EnvBase):
+    """The reference's single-env gym surface on a B = 1 device env."""
+    metadata = {"render.modes": ["human"]}
+
+    def __init__(self, mode):
+        spec = _EnvSpec(mode)
+        self.__dict__.update(spec.__dict__)
+        self._np_rng = np.random
+        self._b = BatchedEnv(mode, 1, seed=0)
+        self.viewer = None
+        self.reset()
+
+    # env.state / env.t / env.episode_step / env.last_goal_dist as numpy views
+    @property
+    def state(self):
+        return self._b.x[0].cpu().numpy().copy()
+
+    @state.setter
+    def state(self, v):
+        self._b.x[0] = torch.as_tensor(np.asarray(v, np.float64), device=self._b.device)
+
+    @property
+    def episode_step(self):
+        return int(self._b.step_count[0].item())
+
+    @episode_step.setter
+    def episode_step(self, v):
+        self._b.step_count[0] = int(v)
+
+    def seed(self, s=None):
+        self.action_space.seed(s)
+        return [s]
+
+    def close(self):
+        pass
+
+    @property
+    def unwrapped(self):
+        return self
+
+    def step(self, action):
+        a = np.asarray(action)
+        if a.dtype not in (np.float32, np.float64):
+            a = a.astype(np.float32)
+        obs32, reward, done, info = self._b.step(torch.as_tensor(a.reshape(1, -1)), auto_reset=False, obs64=True)
+        obs = info["obs64"][0].cpu().numpy()
+        r = reward[0].item()
+        r = np.float32(r) if a.dtype == np.float32 else np.float64(r)
+        return obs, r, bool(done[0].item()), self._info(info)
+
+    def render(self, mode="human", close=False):
+        print("Ep_step = {}, \tState = {}".format(self.episode_step, self.state))
+
+
+class SimulatedCarsEnv(_SingleEnv):
+    """envs/simulated_cars_env.py:6-158 on the device env."""
+
+    def __init__(self):
+        super().__init__("SimulatedCars")
+
+    @property
+    def t(self):
+        return float(self._b.aux[0].item())
+
+    @t.setter
+    def t(self, v):
+        self._b.aux[0] = float(v)
+
+    def reset(self):
+        # the N(0, 0.5) draw comes from the global numpy RNG like the reference (:120)
+        noise = np.array([self._np_rng.normal(0, 0.5)])
+        self._b.reset(noise=noise)
+        return self._get_obs()
+
+    def _get_obs(self):
+        s = self.state
+        o = s.copy()
+        o[::2] /= 100.0
+        o[1::2] /= 30.0
+        return o
+
+    def _info(self, info):
+        return {"cost": float(info["cost"][0].item()), "goal_met": False}
+
+
+class UnicycleEnv(_SingleEnv):
+    """envs/unicycle_env.py:8-280 on the device env (render is out of scope)."""
+
+    def __init__(self):
+        super().__init__("Unicycle")
+
+    @property
+    def last_goal_dist(self):
+        return float(self._b.aux[0].item())
+
+    @last_goal_dist.setter
+    def last_goal_dist(self, v):
+        self._b.aux[0] = float(v)
+
+    def _goal_dist(self):
+        return float(np.linalg.norm(self.goal_pos - self.state[:2]))
+
+    def reset(self):
+        self._b.reset()
+        return self.get_obs()
+
+    def get_obs(self):
+        s = self.state
+        rel = self.goal_pos - s[:2]
+        gd = np.linalg.norm(rel)
+        c, sn = np.cos(s[2]), np.sin(s[2])
+        v = np.matmul(rel, np.array([[c, -sn], [sn, c]]))
+        v /= np.sqrt(np.sum(np.square(v))) + 0.001
+        return np.array([s[0], s[1], c, sn, v[0], v[1], np.exp(-gd)])
+
+    def goal_met(self):
+        return np.linalg.norm(self.state[:2] - self.goal_pos) <= self.goal_size
+
+    def _info(self, info):
+        out = {}
+        if bool(info["goal_met"][0].item()):
+            out["goal_met"] = True
+        c = float(info["cost"][0].item())
+        if c > 0:
+            out["cost"] = c
+        return out

@@ -1,0 +1,88 @@
+"""CPU-side checks of the C-ABI library (no GPU compute): it loads, exports
+every entry point include/rcbf_hip.h declares, and the ctypes mirror of
+rcbf_params has the compiled size; plus host-side argument validation."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "rcbf_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|const char\*)\s+(rcbf_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_path_entry_points():
+    fns = header_functions()
+    for f in ("rcbf_build", "rcbf_qp_solve", "rcbf_safe_action", "rcbf_safe_action_backward",
+              "rcbf_env_step", "rcbf_safe_step", "rcbf_cascade_u_safe", "rcbf_env_reset", "rcbf_safe_rollout"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from rcbf_amd import _lib
+    lib = _lib.load()
+    for f in header_functions():
+        assert hasattr(lib, f), f
+        assert f in _lib.SIGNATURES, f"ctypes binding missing for {f}"
+
+
+def test_params_struct_size_and_abi():
+    from rcbf_amd import _lib
+    lib = _lib.load()
+    assert lib.rcbf_abi_version() == _lib.ABI_VERSION
+    assert lib.rcbf_params_size() == ctypes.sizeof(_lib.RcbfParams)
+    assert b"gfx950" in lib.rcbf_version()
+
+
+def test_argument_validation_without_gpu():
+    """Bad arguments are rejected on the host before any launch."""
+    from rcbf_amd import _lib
+    lib = _lib.load()
+    p = _lib.RcbfParams()
+    p.mode = 7
+    assert lib.rcbf_safe_action(ctypes.byref(p), 4, None, None, None, None, None, None, None, None) == 1001
+    p.mode = _lib.MODE_UNICYCLE
+    p.num_hazards = 0
+    assert lib.rcbf_safe_action(ctypes.byref(p), 4, None, None, None, None, None, None, None, None) == 1002
+    p.num_hazards = 3
+    assert lib.rcbf_safe_action(ctypes.byref(p), 4, None, None, None, None, None, None, None, None) == 1003
+    assert lib.rcbf_safe_action(ctypes.byref(p), -1, None, None, None, None, None, None, None, None) == 1002
+    # empty batch is a no-op
+    assert lib.rcbf_safe_action(ctypes.byref(p), 0, None, None, None, None, None, None, None, None) == 0
+    assert lib.rcbf_qp_solve(ctypes.byref(p), 4, 4, 4, None, None, None, None, 1, None, None, None, None, None) == 1002
+
+
+def test_params_from_env_attributes():
+    from rcbf_amd import _lib
+    from rcbf_amd.envs import _EnvSpec
+    from rcbf_amd.params import make_params
+    spec = _EnvSpec("Unicycle")
+    p = make_params(spec, 40.0, k_d=3.0, l_p=0.05)
+    assert p.mode == _lib.MODE_UNICYCLE and p.num_hazards == 5
+    assert p.hazards_xy[2] == -1.5 and p.hazards_xy[3] == 1.5 and p.hazards_radius == 0.6
+    assert p.u_min[0] == -2.5 and p.u_max[1] == 2.5 and p.l_p == 0.05 and p.k_d == 3.0
+    spec = _EnvSpec("SimulatedCars")
+    p = make_params(spec, 20.0)
+    assert p.mode == _lib.MODE_SIMULATED_CARS and p.kp == 4.0 and p.k_brake == 20.0
+    assert p.u_min[0] == -10.0 and p.u_max[0] == 10.0
+
+    class Bad:
+        dynamics_mode = "SafetyGym"
+
+    with pytest.raises(Exception, match="Dynamics mode not supported."):
+        make_params(Bad(), 1.0)
+
+
+def test_layer_requires_device():
+    """No silent CPU fallback: without a HIP device the product path raises."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        BatchedSimulatedCarsEnv(4)
