@@ -1,0 +1,38 @@
+#!/usr/bin/env bash
+# One GPU-box session: each GPU step under its own time limit; a fault,
+# abort, segfault or time-out ends the session (no further GPU step).
+# Usage: bash scripts/gpu_session.sh TAG step [step ...]
+#   steps: smoke | pytest | bench | prof | pmc | benchx
+set -u
+TAG=${1:?tag}; shift
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+log() { echo "[$(date +%H:%M:%S)] $*" | tee -a "$OUT/steps.log"; }
+run() {
+  local name=$1 lim=$2; shift 2
+  log "start $name"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  log "end $name rc=$rc"
+  case $rc in 124|137|134|139|143) log "fatal rc=$rc, stopping"; exit $rc;; esac
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    smoke)  run smoke 400 python __graft_entry__.py smoke ;;
+    pytest) run pytest 900 python -m pytest tests -m gpu -q -rf -p no:cacheprovider ;;
+    bench)  run bench 600 python bench.py ;;
+    benchu) run benchu 600 python bench.py --env Unicycle --hazards 3 --no-cpu-baseline ;;
+    benchx) run benchx 600 python bench.py --extra --no-cpu-baseline ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+              python3 bench.py --no-cpu-baseline ;;
+    pmcf)   run pmcf 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+              python3 bench.py --no-cpu-baseline --steps 50 --warmup 5 ;;
+    pmcw)   run pmcw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+              python3 bench.py --no-cpu-baseline --steps 50 --warmup 5 ;;
+    *) log "unknown step $step" ;;
+  esac
+done
+log "session done"
