@@ -61,38 +61,38 @@ def largest_divisor_le(n, cap):
 
 
 def cpu_baseline(env_name, hazards, seconds):
-    """The numpy oracle's fused step (oracle/oracle.py) on the host, bounded
-    to ~`seconds`: build + exact QP + clamp + env step per env."""
+    """The C oracle's fused step (oracle/rcbf_oracle.c: build + exact QP +
+    clamp + env step, OpenMP over envs) on this host's cores, on a bounded
+    sample of the same workload (65536 envs, prior mean/sigma), ~`seconds`
+    in total: first 1 thread, then all threads OMP_NUM_THREADS allows."""
+    from oracle import c_oracle as C
     from oracle import oracle as O
-    B = 16384
+    B = 65536
     rng = np.random.default_rng(0)
-    if env_name == "SimulatedCars":
-        x, t, st = O.cars_reset(rng.normal(0, 0.5, B))
-        mu, sg = O.predict_disturbance_prior("SimulatedCars", B)
-        mu, sg = mu.astype(np.float32), sg.astype(np.float32)
-    else:
-        x, ld, st = O.uni_reset(B)
-        hz = O.UNI["hazards"][:hazards]
-        mu, sg = np.zeros((B, 3), np.float32), np.full((B, 3), 0.2, np.float32)
-    n = 0
-    t0 = time.perf_counter()
-    while True:
+    hz = O.UNI["hazards"][:hazards] if env_name == "Unicycle" else None
+    threads_all = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+
+    def run(threads, budget):
         if env_name == "SimulatedCars":
-            u = rng.uniform(-1, 1, (B, 1)).astype(np.float32)
-            s32 = O.get_state_f32("SimulatedCars", O.cars_obs(x).astype(np.float32))
-            fin, _ = O.safe_action_diff("SimulatedCars", s32, u, mu, sg, 20.0)
-            x, t, st, *_ = O.cars_step(x, t, st, fin)
+            x, aux, st = O.cars_reset(rng.normal(0, 0.5, B))
         else:
-            u = rng.uniform(-1, 1, (B, 2)).astype(np.float32)
-            s32 = O.get_state_f32("Unicycle", O.uni_obs(x).astype(np.float32))
-            fin, _ = O.safe_action_diff("Unicycle", s32, u, mu, sg, 20.0, hazards=hz)
-            x, ld, st, *_ = O.uni_step(x, ld, st, fin, hazards=hz)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 1000:
-            break
-    return {"value": round(n * B / el, 1), "unit": "safe env steps/s", "cores": 1, "kind": "port",
-            "sample": f"numpy oracle fused step, {n} steps x {B} envs ({el:.1f} s), 1 thread"}
+            x, aux, st = O.uni_reset(B)
+        st = st.astype(np.int32)
+        n_u = 1 if env_name == "SimulatedCars" else 2
+        u = rng.uniform(-1, 1, (B, n_u)).astype(np.float32)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            C.safe_step(env_name, x, aux, st, u, 20.0, hazards=hz, threads=threads)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget or n >= 10000:
+                return n * B / el, n, el
+
+    v1, n1, e1 = run(1, seconds * 0.3)
+    vN, nN, eN = run(threads_all, seconds * 0.7)
+    return {"value": round(vN, 1), "unit": "safe env steps/s", "cores": threads_all, "kind": "port",
+            "sample": f"C oracle fused step (oracle/rcbf_oracle.c, exact QP), {nN} steps x {B} envs in "
+                      f"{eN:.1f} s on {threads_all} threads; 1 thread: {v1:.4g} steps/s ({n1} steps)"}
 
 
 def main():

@@ -1,0 +1,68 @@
+"""ctypes wrapper of oracle/_build/librcbf_oracle.so -- TEST INFRASTRUCTURE ONLY
+(tests/ and bench.py's cpu_baseline leg).  Same algorithm as oracle.py in C,
+OpenMP over envs; built by __graft_entry__.build_oracle()."""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(_HERE, "_build", "librcbf_oracle.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO):
+            import subprocess
+            import sys
+            subprocess.run([sys.executable, os.path.join(os.path.dirname(_HERE), "__graft_entry__.py"), "build_oracle"],
+                           check=True)
+        _lib = ctypes.CDLL(SO)
+        P = ctypes.c_void_p
+        _lib.oracle_safe_action.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double, ctypes.c_int64,
+                                            P, P, P, P, P, ctypes.c_int]
+        _lib.oracle_safe_step.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double, ctypes.c_int64,
+                                          P, P, P, P, P, P, P, P, ctypes.c_int]
+        _lib.oracle_max_threads.restype = ctypes.c_int
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _hz(hazards):
+    if hazards is None:
+        return np.zeros(2), 0
+    h = np.ascontiguousarray(np.asarray(hazards, np.float64).reshape(-1, 2))
+    return h, h.shape[0]
+
+
+def safe_action(mode, x, u, mu, sigma, gamma_b, hazards=None, threads=0):
+    m = 0 if mode == "SimulatedCars" else 1
+    x = np.ascontiguousarray(x, np.float32); u = np.ascontiguousarray(u, np.float32)
+    mu = np.ascontiguousarray(mu, np.float32); sigma = np.ascontiguousarray(sigma, np.float32)
+    hz, K = _hz(hazards)
+    out = np.empty_like(u)
+    fails = lib().oracle_safe_action(m, K, _p(hz), float(gamma_b), x.shape[0], _p(x), _p(u), _p(mu), _p(sigma),
+                                     _p(out), int(threads))
+    return out, fails
+
+
+def safe_step(mode, x, aux, step, u, gamma_b, hazards=None, threads=0):
+    """In-place fused step on x (B,n_s) f64, aux (B,) f64, step (B,) i32."""
+    m = 0 if mode == "SimulatedCars" else 1
+    u = np.ascontiguousarray(u, np.float32)
+    hz, K = _hz(hazards)
+    B = x.shape[0]
+    uo = np.empty_like(u)
+    rew = np.empty(B, np.float32); cost = np.empty(B, np.float32); done = np.empty(B, np.uint8)
+    fails = lib().oracle_safe_step(m, K, _p(hz), float(gamma_b), B, _p(x), _p(aux), _p(step), _p(u), _p(uo),
+                                   _p(rew), _p(cost), _p(done), int(threads))
+    return uo, rew, cost, done, fails
+
+
+def max_threads():
+    return lib().oracle_max_threads()

@@ -356,9 +356,11 @@ def test_large_batch_properties():
     lam = torch.empty(B, 4, dtype=torch.float64, device="cuda")
     stt = torch.empty(B, dtype=torch.int32, device="cuda")
     import ctypes
-    rc = _lib.load().rcbf_qp_solve(ctypes.byref(layer._prm), B, 2, 4, _lib.ptr(P), _lib.ptr(q), _lib.ptr(dev(Gn)),
-                                   _lib.ptr(dev(hn)), 0, _lib.ptr(zb), _lib.ptr(lam), _lib.ptr(stt), None,
+    Gd, hd = dev(Gn), dev(hn)  # keep the device copies alive until the kernel has run
+    rc = _lib.load().rcbf_qp_solve(ctypes.byref(layer._prm), B, 2, 4, _lib.ptr(P), _lib.ptr(q), _lib.ptr(Gd),
+                                   _lib.ptr(hd), 0, _lib.ptr(zb), _lib.ptr(lam), _lib.ptr(stt), None,
                                    _lib.stream_of(torch.device("cuda")))
+    torch.cuda.synchronize()
     assert rc == 0 and int(stt.max().item()) == 0
     z = zb.double().cpu().numpy(); lm = lam.cpu().numpy()
     Pd = np.array([np.float32(0.1), np.float32(10.0)], np.float64)
