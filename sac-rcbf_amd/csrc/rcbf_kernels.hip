@@ -15,7 +15,18 @@ using namespace rcbf;
 
 namespace {
 
-constexpr int kBlock = 256;
+#ifndef RCBF_BLOCK
+#define RCBF_BLOCK 256
+#endif
+constexpr int kBlock = RCBF_BLOCK;
+// Ablation switches for performance studies only (scripts/ablate.sh builds
+// them into separate libraries; the product build uses 0):
+//   1 = no QP (u_qp = 0), 2 = no rows/normalise/QP, 4 = no env dynamics,
+//   8 = no observation maths
+#ifndef RCBF_ABLATE
+#define RCBF_ABLATE 0
+#endif
+constexpr int kAblate = RCBF_ABLATE;
 
 inline unsigned grid_for(int64_t B) { return (unsigned)((B + kBlock - 1) / kBlock); }
 
@@ -97,6 +108,12 @@ __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const floa
                                               const float* mu, const float* sig, float* u_final,
                                               LayerState<MODE, K>& L) {
     using D = Dims<MODE, K>;
+    if constexpr ((kAblate & 2) != 0) {
+#pragma unroll
+        for (int c = 0; c < D::NU; ++c) u_final[c] = u[c] + xs[c] * 1e-30f;
+        L.qp.status = RCBF_QP_OK;
+        return;
+    }
     diff_rows<MODE, K>(prm, xs, u, mu, sig, L.G, L.h);
 #pragma unroll
     for (int r = 0; r < D::M; ++r) {
@@ -111,7 +128,13 @@ __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const floa
 #pragma unroll
     for (int k = 0; k < D::N; ++k) q[k] = 0.0;
     pmat_set_diag<D::N>(pm, pd);
-    qp_solve<D::N, D::M, true, float>(prm.solver, pm, q, L.G, L.h, prm.max_iter, prm.eps, L.qp);
+    if constexpr ((kAblate & 1) != 0) {
+#pragma unroll
+        for (int k = 0; k < D::N; ++k) L.qp.z[k] = 1e-30 * (double)(L.G[0][k] + L.h[k % D::M]);
+        L.qp.status = RCBF_QP_OK;
+    } else {
+        qp_solve<D::N, D::M, true, float>(prm.solver, pm, q, L.G, L.h, prm.max_iter, prm.eps, L.qp);
+    }
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) {
         float v = u[c] + (float)L.qp.z[c];
@@ -487,7 +510,10 @@ __device__ __forceinline__ void env_reset_one(const double* noise, int64_t i, ui
 
 template <int MODE>
 __device__ __forceinline__ void env_obs(const double* xs, double* o) {
-    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS)
+    if constexpr ((kAblate & 8) != 0) {
+#pragma unroll
+        for (int k = 0; k < Dims<MODE, 1>::NO; ++k) o[k] = xs[k % Dims<MODE, 1>::NS];
+    } else if constexpr (MODE == RCBF_MODE_SIMULATED_CARS)
         cars_obs(xs, o);
     else
         uni_obs(xs, o);
@@ -603,7 +629,15 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
     LayerState<MODE, K> L;
     layer_forward<MODE, K>(prm, s32, us, m, s, uf, L);
     status = L.qp.status;
-    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+    if constexpr ((kAblate & 4) != 0) {
+#pragma unroll
+        for (int k = 0; k < D::NS; ++k) xs[k] += 1e-3 * (double)uf[0];
+        st += 1;
+        rew = uf[0];
+        cst = 0.0f;
+        dn = st >= 300;
+        gm = false;
+    } else if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
         CarsStepOut o;
         cars_env_step<float>(prm, xs, a, st, uf[0], o);
         rew = o.reward;
