@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 2
+#define RCBF_ABI_VERSION 3
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -43,8 +43,9 @@ extern "C" {
 #define RCBF_FORM_CASCADE 1 /* CascadeCBFLayer, rcbf_sac/cbf_qp.py (fp64 rows, fp64 QP) */
 
 /* QP solvers */
-#define RCBF_SOLVER_ACTIVE_SET 0 /* Goldfarb-Idnani dual active set, fp64 (quadprog's algorithm, exact) */
-#define RCBF_SOLVER_PDIPM 1      /* primal-dual interior point, fp64 (qpth's algorithm family)        */
+#define RCBF_SOLVER_ACTIVE_SET 0 /* exact, fp64: KKT enumeration (n=2) / Goldfarb-Idnani (n=3)          */
+#define RCBF_SOLVER_PDIPM 1      /* primal-dual interior point, fp64 (qpth's algorithm family) + polish */
+#define RCBF_SOLVER_GI 2         /* Goldfarb-Idnani dual active set for every n (quadprog's algorithm) */
 
 /* per-QP status codes */
 #define RCBF_QP_OK 0
@@ -134,9 +135,12 @@ int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom,
 /* ---------------------------------------------------------------------- */
 /* Environments (batched, device-resident, fp64 state like the numpy envs) */
 /* ---------------------------------------------------------------------- */
-/* Per-env state:  x (B, n_s) f64 = env.state;  aux (B,) f64 = env.t (cars)
- * or env.last_goal_dist (unicycle);  step (B,) i32 = env.episode_step;
- * episode (B,) u32 = reset counter keying the per-env counter-based RNG.  */
+/* Per-env state, COMPONENT-MAJOR (SoA):  x (n_s, B) f64, x[k*B + i] =
+ * env_i.state[k];  aux (B,) f64 = env.t (cars) or env.last_goal_dist
+ * (unicycle);  step (B,) i32 = env.episode_step;  episode (B,) u32 = reset
+ * counter keying the per-env counter-based RNG (read/written only on reset).
+ * Observations are row-major (B, n_o), the policy's input layout, 8-byte
+ * aligned.  (For B = 1 the SoA and row-major layouts coincide.)  */
 
 /* SimulatedCarsEnv.reset (simulated_cars_env.py:108-125) / UnicycleEnv.reset
  * (unicycle_env.py:125-143) for the envs selected by mask [nullable: all].

@@ -1,0 +1,287 @@
+// rcbf_common.hpp -- pieces shared by the three kernel translation units
+// (rcbf_layer.hip, rcbf_qp.hip, rcbf_env.hip): mode traits, the fused
+// CBFQPLayer forward for one env, env helpers, launch/dispatch helpers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rcbf_device.hpp"
+
+namespace rcbf {
+
+#ifndef RCBF_BLOCK
+#define RCBF_BLOCK 256
+#endif
+constexpr int kBlock = RCBF_BLOCK;
+// Ablation switches for performance studies only (scripts/build_variants.sh
+// builds them into separate libraries; the product build uses 0):
+//   1 = no QP (u_qp = 0), 2 = no rows/normalise/QP, 4 = no env dynamics,
+//   8 = no observation maths
+#ifndef RCBF_ABLATE
+#define RCBF_ABLATE 0
+#endif
+constexpr int kAblate = RCBF_ABLATE;
+
+inline unsigned grid_for(int64_t B) { return (unsigned)((B + kBlock - 1) / kBlock); }
+
+// ---------------------------------------------------------------------------
+// mode traits
+// ---------------------------------------------------------------------------
+template <int MODE, int K>
+struct Dims;
+template <int K>
+struct Dims<RCBF_MODE_SIMULATED_CARS, K> {
+    static constexpr int NS = 10, NU = 1, N = 2, M = 4, NO = 10;
+};
+template <int K>
+struct Dims<RCBF_MODE_UNICYCLE, K> {
+    static constexpr int NS = 3, NU = 2, N = 3, M = K + 4, NO = 7;
+};
+
+// prior disturbance (dynamics.py:24, 381-384): mean 0, sigma = MAX_STD cast to fp32
+template <int MODE>
+__device__ __forceinline__ float prior_sigma(int k) {
+    if (MODE == RCBF_MODE_SIMULATED_CARS) return (k & 1) ? (float)0.2 : 0.0f;
+    return (float)0.2;
+}
+
+// P of the diff layer, as the fp32 tensor qpth receives then casts to fp64
+// (diff_cbf_qp.py:265,356,139)
+template <int MODE>
+__device__ __forceinline__ void diff_P(double* d) {
+    if (MODE == RCBF_MODE_SIMULATED_CARS) {
+        d[0] = (double)0.1f;
+        d[1] = (double)10.0f;
+    } else {
+        d[0] = (double)1.0f;
+        d[1] = (double)1e-2f;
+        d[2] = (double)1e5f;
+    }
+}
+
+// P of the Cascade layer (cbf_qp.py:146, 218), fp64
+template <int MODE>
+__device__ __forceinline__ void cascade_P(double* d) {
+    if (MODE == RCBF_MODE_SIMULATED_CARS) {
+        d[0] = 0.1;
+        d[1] = 1e1;
+    } else {
+        d[0] = 1.e1;
+        d[1] = 1.e-4;
+        d[2] = 1e7;
+    }
+}
+
+template <int MODE, int K>
+__device__ __forceinline__ void diff_rows(const rcbf_params& prm, const float* xs, const float* u,
+                                          const float* mu, const float* sig,
+                                          float (*G)[Dims<MODE, K>::N], float* h) {
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+        cars_rows_diff(prm, xs, u[0], sig[5], sig[7], sig[9], G, h);
+    } else {
+        uni_rows_diff<K>(prm, xs, u, mu, sig, G, h);
+    }
+}
+
+// What one env's CBFQPLayer forward leaves behind (the backward re-uses it).
+template <int MODE, int K>
+struct LayerState {
+    using D = Dims<MODE, K>;
+    float G[D::M][D::N];  // normalised rows (what qpth sees)
+    float h[D::M];
+    float Graw[D::M][D::N];
+    float hraw[D::M];
+    float Nrm[D::M];
+    bool ish[D::M];
+    QPResult<D::N, D::M> qp;
+};
+
+// CBFQPLayer.get_safe_action for one env (diff_cbf_qp.py:44-79):
+// build -> normalise -> fp64 QP -> .float() -> clamp.
+template <int SOLVER, int MODE, int K>
+__device__ __forceinline__ void layer_forward(const rcbf_params& prm, const float* xs, const float* u,
+                                              const float* mu, const float* sig, float* u_final,
+                                              LayerState<MODE, K>& L) {
+    using D = Dims<MODE, K>;
+    if constexpr ((kAblate & 2) != 0) {
+#pragma unroll
+        for (int c = 0; c < D::NU; ++c) u_final[c] = u[c] + xs[c] * 1e-30f;
+        L.qp.status = RCBF_QP_OK;
+        return;
+    }
+    diff_rows<MODE, K>(prm, xs, u, mu, sig, L.G, L.h);
+#pragma unroll
+    for (int r = 0; r < D::M; ++r) {
+        L.hraw[r] = L.h[r];
+#pragma unroll
+        for (int k = 0; k < D::N; ++k) L.Graw[r][k] = L.G[r][k];
+    }
+    normalize_rows<D::N, D::M, float>(L.G, L.h, L.Nrm, L.ish);
+    PMat<D::N, true> pm;
+    double pd[D::N], q[D::N];
+    diff_P<MODE>(pd);
+#pragma unroll
+    for (int k = 0; k < D::N; ++k) q[k] = 0.0;
+    pmat_set_diag<D::N>(pm, pd);
+    if constexpr ((kAblate & 1) != 0) {
+#pragma unroll
+        for (int k = 0; k < D::N; ++k) L.qp.z[k] = 1e-30 * (double)(L.G[0][k] + L.h[k % D::M]);
+        L.qp.status = RCBF_QP_OK;
+    } else {
+        qp_solve<SOLVER, D::N, D::M, true, float>(pm, q, L.G, L.h, prm.max_iter, prm.eps, L.qp);
+    }
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) {
+        float v = u[c] + (float)L.qp.z[c];
+        float lo = (float)prm.u_min[c], hi = (float)prm.u_max[c];
+        u_final[c] = fminf(fmaxf(v, lo), hi);  // torch.clamp (diff_cbf_qp.py:77)
+    }
+}
+
+__device__ __forceinline__ void report(int status, int32_t* status_out, int64_t i, int32_t* fail_flag) {
+    if (status_out) status_out[i] = status;
+    if (status != RCBF_QP_OK && fail_flag) atomicOr(fail_flag, 1 << status);
+}
+
+// ---------------------------------------------------------------------------
+// environments
+// ---------------------------------------------------------------------------
+// Env state in HBM is component-major (SoA): x[k * B + i] is component k of
+// env i, so every component load/store of a wavefront is one contiguous
+// 512-byte access.  aux/step/episode are (B,) vectors.
+template <int MODE>
+__device__ __forceinline__ void env_reset_one(const double* noise, int64_t i, uint64_t seed, int64_t off,
+                                              uint32_t ep, double* xs, double& aux, int& st) {
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+        double nz = noise ? noise[i] : 0.5 * normal_draw(seed, (uint64_t)(off + i), ep);
+        cars_reset_state(xs, nz);
+        aux = 0.0;
+    } else {
+        uni_reset_state(xs, aux);
+    }
+    st = 0;
+}
+
+template <int MODE>
+__device__ __forceinline__ void env_obs(const double* xs, double* o) {
+    if constexpr ((kAblate & 8) != 0) {
+#pragma unroll
+        for (int k = 0; k < Dims<MODE, 1>::NO; ++k) o[k] = xs[k % Dims<MODE, 1>::NS];
+    } else if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+        cars_obs(xs, o);
+    } else {
+        uni_obs(xs, o);
+    }
+}
+
+// state32 = get_state(float(obs(x)))   (dynamics.py:190-232, via the fp32
+// observation the policy sees: sac_cbf.py:61 then to_numpy/fp64/rescale/fp32)
+template <int MODE>
+__device__ __forceinline__ void state_from_env(const double* xs, float* s32) {
+#pragma clang fp contract(off)
+    double o[Dims<MODE, 1>::NO];
+    env_obs<MODE>(xs, o);
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) s32[k] = (float)((double)(float)o[k] * ((k & 1) ? 30.0 : 100.0));
+    } else {
+        s32[0] = (float)o[0];
+        s32[1] = (float)o[1];
+        s32[2] = (float)atan2((double)(float)o[3], (double)(float)o[2]);
+    }
+}
+
+// One fused safe step for one env (shared by k_safe_step and k_safe_rollout).
+// The episode counter is only touched when the env resets.
+template <int SOLVER, int MODE, int K>
+__device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i, double* xs, double& a, int& st,
+                                              uint32_t* episode, const float* us, const float* m, const float* s,
+                                              float* uf, float& rew, float& cst, bool& dn, bool& gm, int& status,
+                                              int auto_reset, uint64_t seed, int64_t off) {
+    using D = Dims<MODE, K>;
+    float s32[D::NS];
+    state_from_env<MODE>(xs, s32);
+    LayerState<MODE, K> L;
+    layer_forward<SOLVER, MODE, K>(prm, s32, us, m, s, uf, L);
+    status = L.qp.status;
+    if constexpr ((kAblate & 4) != 0) {
+#pragma unroll
+        for (int k = 0; k < D::NS; ++k) xs[k] += 1e-3 * (double)uf[0];
+        st += 1;
+        rew = uf[0];
+        cst = 0.0f;
+        dn = st >= 300;
+        gm = false;
+    } else if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+        CarsStepOut o;
+        cars_env_step<float>(prm, xs, a, st, uf[0], o);
+        rew = o.reward;
+        cst = (float)o.cost;
+        dn = o.done;
+        gm = false;
+    } else {
+        UniStepOut o;
+        uni_env_step<float>(prm, xs, a, st, uf, o);
+        rew = (float)o.reward;
+        cst = (float)o.cost;
+        dn = o.done;
+        gm = o.goal;
+    }
+    if (auto_reset && dn) {
+        uint32_t ep = episode ? episode[i] + 1u : 0u;
+        if (episode) episode[i] = ep;
+        env_reset_one<MODE>(nullptr, i, seed, off, ep, xs, a, st);
+    }
+}
+
+inline int check_prm(const rcbf_params* prm) {
+    if (!prm) return RCBF_E_NULL;
+    if (prm->mode != RCBF_MODE_SIMULATED_CARS && prm->mode != RCBF_MODE_UNICYCLE) return RCBF_E_BAD_MODE;
+    if (prm->mode == RCBF_MODE_UNICYCLE && (prm->num_hazards < 1 || prm->num_hazards > RCBF_MAX_HAZARDS))
+        return RCBF_E_BAD_SHAPE;
+    if (prm->solver != RCBF_SOLVER_ACTIVE_SET && prm->solver != RCBF_SOLVER_PDIPM && prm->solver != RCBF_SOLVER_GI)
+        return RCBF_E_BAD_MODE;
+    return 0;
+}
+
+inline int launch_status() { return (int)hipGetLastError(); }
+
+}  // namespace rcbf
+
+// Dispatch a launch over (mode, unicycle hazard count) -> MODE_, K_.
+#define RCBF_DISPATCH_MODE(prm, ...)                                 \
+    do {                                                             \
+        if ((prm)->mode == RCBF_MODE_SIMULATED_CARS) {               \
+            constexpr int MODE_ = RCBF_MODE_SIMULATED_CARS;          \
+            constexpr int K_ = 1;                                    \
+            __VA_ARGS__;                                             \
+        } else {                                                     \
+            constexpr int MODE_ = RCBF_MODE_UNICYCLE;                \
+            switch ((prm)->num_hazards) {                            \
+                case 1: { constexpr int K_ = 1; __VA_ARGS__; } break; \
+                case 2: { constexpr int K_ = 2; __VA_ARGS__; } break; \
+                case 3: { constexpr int K_ = 3; __VA_ARGS__; } break; \
+                case 4: { constexpr int K_ = 4; __VA_ARGS__; } break; \
+                case 5: { constexpr int K_ = 5; __VA_ARGS__; } break; \
+                case 6: { constexpr int K_ = 6; __VA_ARGS__; } break; \
+                case 7: { constexpr int K_ = 7; __VA_ARGS__; } break; \
+                default: { constexpr int K_ = 8; __VA_ARGS__; } break; \
+            }                                                        \
+        }                                                            \
+    } while (0)
+
+// ... and over the solver -> SOLVER_.
+#define RCBF_DISPATCH(prm, ...)                                                        \
+    do {                                                                               \
+        if ((prm)->solver == RCBF_SOLVER_PDIPM) {                                      \
+            constexpr int SOLVER_ = RCBF_SOLVER_PDIPM;                                 \
+            RCBF_DISPATCH_MODE(prm, __VA_ARGS__);                                      \
+        } else if ((prm)->solver == RCBF_SOLVER_GI) {                                  \
+            constexpr int SOLVER_ = RCBF_SOLVER_GI;                                    \
+            RCBF_DISPATCH_MODE(prm, __VA_ARGS__);                                      \
+        } else {                                                                       \
+            constexpr int SOLVER_ = RCBF_SOLVER_ACTIVE_SET;                            \
+            RCBF_DISPATCH_MODE(prm, __VA_ARGS__);                                      \
+        }                                                                              \
+    } while (0)

@@ -737,14 +737,119 @@ __device__ __forceinline__ void pdipm_solve(const PMat<N, DIAG>& pm, const doubl
     out.iters = it;
 }
 
-template <int N, int M, bool DIAG, typename R>
-__device__ __forceinline__ void qp_solve(int solver, const PMat<N, DIAG>& pm, const double* q,
-                                         const R (*G)[N], const R* h, int max_iter, double eps,
-                                         QPResult<N, M>& out) {
-    if (solver == RCBF_SOLVER_PDIPM)
+// Exact solver for n = 2 variables (the cars QP, z = [u, eps]) with diagonal P
+// and q = 0: enumerate the KKT candidates of every row subset of size <= 2
+// (the unconstrained minimum, the minimiser on each row's hyperplane, each
+// pair's vertex) and keep the primal-feasible one with the smallest
+// objective.  The optimum is one of the candidates (it minimises the
+// objective on the affine hull of its active set) and is feasible; every
+// other feasible candidate has an objective at least as large, so no dual
+// test is needed.  All candidates are independent: ~1 + M + M(M-1)/2 short
+// fp64 expressions with no loop-carried dependency, which suits a single
+// wave per SIMD far better than an iterative active-set loop.
+template <int M, typename R>
+__device__ __forceinline__ void enum2_solve(const PMat<2, true>& pm, const R (*G)[2], const R* h,
+                                            QPResult<2, M>& out) {
+    const double pi0 = pm.Pinv[0][0], pi1 = pm.Pinv[1][1];
+    const double p0 = pm.P[0][0], p1 = pm.P[1][1];
+    double g0[M], g1[M], hh[M];
+    bool finite = true;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        g0[r] = (double)G[r][0];
+        g1[r] = (double)G[r][1];
+        hh[r] = (double)h[r];
+        finite = finite && isfinite(g0[r]) && isfinite(g1[r]) && isfinite(hh[r]);
+    }
+    double best = kInf, bz0 = 0.0, bz1 = 0.0;
+    uint32_t bact = 0;
+    auto consider = [&](double z0, double z1, uint32_t act, bool valid) {
+        bool feas = valid;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            double v = fma(g0[r], z0, fma(g1[r], z1, -hh[r]));
+            feas = feas && (v <= 1e-9 * (1.0 + fabs(hh[r])));
+        }
+        double obj = fma(p0 * z0, z0, p1 * z1 * z1);
+        bool take = feas && (obj < best);
+        best = take ? obj : best;
+        bz0 = take ? z0 : bz0;
+        bz1 = take ? z1 : bz1;
+        bact = take ? act : bact;
+    };
+    consider(0.0, 0.0, 0u, true);
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        // z = P^-1 g h / (g P^-1 g')
+        double nrm = fma(g0[r] * pi0, g0[r], g1[r] * pi1 * g1[r]);
+        bool ok = nrm > 1e-300;
+        double f = ok ? hh[r] / nrm : 0.0;
+        consider(pi0 * g0[r] * f, pi1 * g1[r] * f, 1u << r, ok);
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+#pragma unroll
+        for (int s = r + 1; s < M; ++s) {
+            double det = g0[r] * g1[s] - g1[r] * g0[s];
+            bool ok = fabs(det) > 1e-12;
+            double inv = ok ? 1.0 / det : 0.0;
+            double z0 = (hh[r] * g1[s] - hh[s] * g1[r]) * inv;
+            double z1 = (g0[r] * hh[s] - g0[s] * hh[r]) * inv;
+            consider(z0, z1, (1u << r) | (1u << s), ok);
+        }
+    }
+    out.z[0] = bz0;
+    out.z[1] = bz1;
+    // multipliers of the chosen set:  P z + G_A' lam = 0
+    double Pz0 = p0 * bz0, Pz1 = p1 * bz1;
+    int ra = -1, rb = -1;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        bool a = (bact >> r) & 1u;
+        rb = (a && ra >= 0 && rb < 0) ? r : rb;
+        ra = (a && ra < 0) ? r : ra;
+    }
+    double ga0 = 0, ga1 = 0, gb0 = 0, gb1 = 0;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        ga0 = (r == ra) ? g0[r] : ga0;
+        ga1 = (r == ra) ? g1[r] : ga1;
+        gb0 = (r == rb) ? g0[r] : gb0;
+        gb1 = (r == rb) ? g1[r] : gb1;
+    }
+    double la = 0.0, lb = 0.0;
+    if (rb >= 0) {  // [ga gb] [la lb]' = -Pz  (2x2, Cramer)
+        double det = ga0 * gb1 - gb0 * ga1;
+        la = (-Pz0 * gb1 + Pz1 * gb0) / det;
+        lb = (-ga0 * Pz1 + ga1 * Pz0) / det;
+    } else if (ra >= 0) {
+        double nn = ga0 * ga0 + ga1 * ga1;
+        la = -(Pz0 * ga0 + Pz1 * ga1) / nn;
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) out.lam[r] = (r == ra) ? la : ((r == rb) ? lb : 0.0);
+    out.active = bact;
+    out.nact = (ra >= 0) + (rb >= 0);
+    out.iters = 1;
+    bool okz = isfinite(bz0) && isfinite(bz1) && best < kInf;
+    out.status = !finite ? RCBF_QP_NONFINITE : (okz ? RCBF_QP_OK : RCBF_QP_INFEASIBLE);
+}
+
+// Compile-time solver choice (the host dispatches on rcbf_params.solver):
+//   RCBF_SOLVER_ACTIVE_SET: exact -- KKT enumeration for n = 2, Goldfarb-Idnani
+//                           for n = 3 or a full P;
+//   RCBF_SOLVER_GI:         Goldfarb-Idnani for every size;
+//   RCBF_SOLVER_PDIPM:      primal-dual interior point + active-set polish.
+template <int SOLVER, int N, int M, bool DIAG, typename R>
+__device__ __forceinline__ void qp_solve(const PMat<N, DIAG>& pm, const double* q, const R (*G)[N],
+                                         const R* h, int max_iter, double eps, QPResult<N, M>& out) {
+    if constexpr (SOLVER == RCBF_SOLVER_PDIPM) {
         pdipm_solve<N, M, DIAG, R>(pm, q, G, h, max_iter > 0 ? max_iter : 50, eps > 0 ? eps : 1e-10, out);
-    else
+    } else if constexpr (SOLVER == RCBF_SOLVER_ACTIVE_SET && N == 2 && DIAG) {
+        enum2_solve<M, R>(pm, G, h, out);
+    } else {
         gi_solve<N, M, DIAG, R>(pm, q, G, h, max_iter > 0 ? max_iter : 4 * (M + N) + 8, out);
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,287 @@
+// rcbf_env.hip -- device-resident environments and the fused safe step + C-ABI:
+// rcbf_env_reset, rcbf_env_step, rcbf_safe_step (the hot path bench.py
+// measures), rcbf_safe_rollout, version/ABI queries.
+//
+// Env state is component-major (SoA) in HBM: x[k * B + i].  One env per
+// lane; a wavefront's load or store of one component is a contiguous 512 B
+// (f64) or 256 B (f32) access.  The fused step reads x, t, step, u_RL and
+// writes x', t', step', obs (AoS, the policy's (B, n_o) input), u, reward,
+// cost, done; the episode counter is touched only on resets.
+#include "rcbf_common.hpp"
+
+using namespace rcbf;
+
+namespace {
+
+template <int MODE>
+__device__ __forceinline__ void load_state(const double* x, int64_t B, int64_t i, double* xs) {
+#pragma unroll
+    for (int k = 0; k < Dims<MODE, 1>::NS; ++k) xs[k] = x[k * B + i];
+}
+
+template <int MODE>
+__device__ __forceinline__ void store_state(double* x, int64_t B, int64_t i, const double* xs) {
+#pragma unroll
+    for (int k = 0; k < Dims<MODE, 1>::NS; ++k) x[k * B + i] = xs[k];
+}
+
+template <int MODE>
+__device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double* xs) {
+    constexpr int NO = Dims<MODE, 1>::NO;
+    double o[NO];
+    env_obs<MODE>(xs, o);
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+        float2* ov = reinterpret_cast<float2*>(obs + i * NO);  // 40 B rows, 8 B aligned
+#pragma unroll
+        for (int k = 0; k < NO / 2; ++k) ov[k] = make_float2((float)o[2 * k], (float)o[2 * k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NO; ++k) obs[i * NO + k] = (float)o[k];
+    }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) k_env_reset(rcbf_params prm, int64_t B, const uint8_t* __restrict__ mask,
+                                                      const double* __restrict__ noise, uint64_t seed, int64_t off,
+                                                      double* __restrict__ x, double* __restrict__ aux,
+                                                      int32_t* __restrict__ step, uint32_t* __restrict__ episode,
+                                                      float* __restrict__ obs_out) {
+    using D = Dims<MODE, 1>;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    if (mask && !mask[i]) return;
+    double xs[D::NS], a;
+    int st;
+    uint32_t ep = episode ? episode[i] + 1u : 0u;
+    env_reset_one<MODE>(noise, i, seed, off, ep, xs, a, st);
+    store_state<MODE>(x, B, i, xs);
+    aux[i] = a;
+    step[i] = st;
+    if (episode) episode[i] = ep;
+    if (obs_out) store_obs32<MODE>(obs_out, i, xs);
+}
+
+template <int MODE, typename A>
+__global__ void __launch_bounds__(kBlock) k_env_step(rcbf_params prm, int64_t B, double* __restrict__ x,
+                                                     double* __restrict__ aux, int32_t* __restrict__ step,
+                                                     uint32_t* __restrict__ episode, const A* __restrict__ action,
+                                                     double* __restrict__ obs64, float* __restrict__ obs32,
+                                                     double* __restrict__ reward, double* __restrict__ cost,
+                                                     uint8_t* __restrict__ done, uint8_t* __restrict__ goal_met,
+                                                     int auto_reset, uint64_t seed, int64_t off) {
+    using D = Dims<MODE, 1>;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    double xs[D::NS];
+    load_state<MODE>(x, B, i, xs);
+    double a = aux[i];
+    int st = step[i];
+    bool dn, gm = false;
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+        CarsStepOut o;
+        cars_env_step<A>(prm, xs, a, st, action[i], o);
+        reward[i] = o.reward_d;
+        cost[i] = o.cost;
+        dn = o.done;
+    } else {
+        A act[2] = {action[2 * i], action[2 * i + 1]};
+        UniStepOut o;
+        uni_env_step<A>(prm, xs, a, st, act, o);
+        reward[i] = o.reward;
+        cost[i] = o.cost;
+        dn = o.done;
+        gm = o.goal;
+    }
+    done[i] = dn;
+    if (goal_met) goal_met[i] = gm;
+    if (auto_reset && dn) {
+        uint32_t ep = episode ? episode[i] + 1u : 0u;
+        env_reset_one<MODE>(nullptr, i, seed, off, ep, xs, a, st);
+        if (episode) episode[i] = ep;
+    }
+    store_state<MODE>(x, B, i, xs);
+    aux[i] = a;
+    step[i] = st;
+    if (obs64) {
+        double o[D::NO];
+        env_obs<MODE>(xs, o);
+#pragma unroll
+        for (int k = 0; k < D::NO; ++k) obs64[i * D::NO + k] = o[k];
+    }
+    if (obs32) store_obs32<MODE>(obs32, i, xs);
+}
+
+template <int SOLVER, int MODE, int K>
+__global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B, double* __restrict__ x,
+                                                      double* __restrict__ aux, int32_t* __restrict__ step,
+                                                      uint32_t* __restrict__ episode, const float* __restrict__ u_rl,
+                                                      const float* __restrict__ mu, const float* __restrict__ sigma,
+                                                      float* __restrict__ obs_out, float* __restrict__ u_out,
+                                                      float* __restrict__ reward, float* __restrict__ cost,
+                                                      uint8_t* __restrict__ done, uint8_t* __restrict__ goal_met,
+                                                      int32_t* __restrict__ status_out, int32_t* fail_flag,
+                                                      int auto_reset, uint64_t seed, int64_t off) {
+    using D = Dims<MODE, K>;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    double xs[D::NS];
+    load_state<MODE>(x, B, i, xs);
+    double a = aux[i];
+    int st = step[i];
+    float us[D::NU], m[D::NS], s[D::NS], uf[D::NU];
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) us[c] = u_rl[i * D::NU + c];
+#pragma unroll
+    for (int k = 0; k < D::NS; ++k) {
+        m[k] = mu ? mu[i * D::NS + k] : 0.0f;
+        s[k] = sigma ? sigma[i * D::NS + k] : prior_sigma<MODE>(k);
+    }
+    float rew, cst;
+    bool dn, gm;
+    int status;
+    safe_step_one<SOLVER, MODE, K>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
+                                   seed, off);
+    store_state<MODE>(x, B, i, xs);
+    aux[i] = a;
+    step[i] = st;
+    store_obs32<MODE>(obs_out, i, xs);
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) u_out[i * D::NU + c] = uf[c];
+    reward[i] = rew;
+    cost[i] = cst;
+    done[i] = dn;
+    if (goal_met) goal_met[i] = gm;
+    report(status, status_out, i, fail_flag);
+}
+
+template <int MODE, int K>
+__global__ void __launch_bounds__(kBlock) k_safe_rollout(rcbf_params prm, int64_t B, int Ksteps,
+                                                         double* __restrict__ x, double* __restrict__ aux,
+                                                         int32_t* __restrict__ step, uint32_t* __restrict__ episode,
+                                                         const float* __restrict__ u_rl, float* __restrict__ obs_out,
+                                                         float* __restrict__ reward_sum, float* __restrict__ cost_sum,
+                                                         int32_t* __restrict__ n_done, int32_t* fail_flag,
+                                                         uint64_t seed, int64_t off) {
+    using D = Dims<MODE, K>;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    double xs[D::NS];
+    load_state<MODE>(x, B, i, xs);
+    double a = aux[i];
+    int st = step[i];
+    float m[D::NS], s[D::NS];
+#pragma unroll
+    for (int k = 0; k < D::NS; ++k) {
+        m[k] = 0.0f;
+        s[k] = prior_sigma<MODE>(k);
+    }
+    float rs = 0.0f, cs = 0.0f;
+    int nd = 0, worst = RCBF_QP_OK;
+    for (int t = 0; t < Ksteps; ++t) {
+        float us[D::NU], uf[D::NU];
+#pragma unroll
+        for (int c = 0; c < D::NU; ++c) us[c] = u_rl[((int64_t)t * B + i) * D::NU + c];
+        float rew, cst;
+        bool dn, gm;
+        int status;
+        safe_step_one<RCBF_SOLVER_ACTIVE_SET, MODE, K>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm,
+                                                       status, 1, seed, off);
+        rs += rew;
+        cs += cst;
+        nd += dn ? 1 : 0;
+        worst = status > worst ? status : worst;
+    }
+    store_state<MODE>(x, B, i, xs);
+    aux[i] = a;
+    step[i] = st;
+    if (obs_out) store_obs32<MODE>(obs_out, i, xs);
+    reward_sum[i] = rs;
+    cost_sum[i] = cs;
+    n_done[i] = nd;
+    if (worst != RCBF_QP_OK && fail_flag) atomicOr(fail_flag, 1 << worst);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rcbf_version(void) { return "rcbf_hip 0.2.0 (gfx950)"; }
+int32_t rcbf_abi_version(void) { return RCBF_ABI_VERSION; }
+int32_t rcbf_params_size(void) { return (int32_t)sizeof(rcbf_params); }
+
+int rcbf_env_reset(const rcbf_params* prm, int64_t B, const uint8_t* mask, const double* noise, uint64_t seed,
+                   int64_t env_offset, double* x, double* aux, int32_t* step, uint32_t* episode, float* obs_out,
+                   hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !aux || !step) return RCBF_E_NULL;
+    if (obs_out && (((uintptr_t)obs_out) & 7)) return RCBF_E_BAD_SHAPE;
+    if (prm->mode == RCBF_MODE_SIMULATED_CARS)
+        hipLaunchKernelGGL((k_env_reset<RCBF_MODE_SIMULATED_CARS>), dim3(grid_for(B)), dim3(kBlock), 0, stream, *prm,
+                           B, mask, noise, seed, env_offset, x, aux, step, episode, obs_out);
+    else
+        hipLaunchKernelGGL((k_env_reset<RCBF_MODE_UNICYCLE>), dim3(grid_for(B)), dim3(kBlock), 0, stream, *prm, B,
+                           mask, noise, seed, env_offset, x, aux, step, episode, obs_out);
+    return launch_status();
+}
+
+int rcbf_env_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
+                  const void* action, int32_t action_f64, double* obs64_out, float* obs_out, double* reward,
+                  double* cost, uint8_t* done, uint8_t* goal_met, int32_t auto_reset, uint64_t seed,
+                  int64_t env_offset, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !aux || !step || !action || !reward || !cost || !done) return RCBF_E_NULL;
+    if (obs_out && (((uintptr_t)obs_out) & 7)) return RCBF_E_BAD_SHAPE;
+    dim3 g(grid_for(B)), b(kBlock);
+#define RCBF_ENV_L(MODE, A)                                                                                       \
+    hipLaunchKernelGGL((k_env_step<MODE, A>), g, b, 0, stream, *prm, B, x, aux, step, episode, (const A*)action, \
+                       obs64_out, obs_out, reward, cost, done, goal_met, auto_reset, seed, env_offset)
+    if (prm->mode == RCBF_MODE_SIMULATED_CARS) {
+        if (action_f64)
+            RCBF_ENV_L(RCBF_MODE_SIMULATED_CARS, double);
+        else
+            RCBF_ENV_L(RCBF_MODE_SIMULATED_CARS, float);
+    } else {
+        if (action_f64)
+            RCBF_ENV_L(RCBF_MODE_UNICYCLE, double);
+        else
+            RCBF_ENV_L(RCBF_MODE_UNICYCLE, float);
+    }
+#undef RCBF_ENV_L
+    return launch_status();
+}
+
+int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
+                   const float* u_rl, const float* mu, const float* sigma, float* obs_out, float* u_out,
+                   float* reward, float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
+                   int32_t* fail_flag, int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !aux || !step || !u_rl || !obs_out || !u_out || !reward || !cost || !done) return RCBF_E_NULL;
+    if (((uintptr_t)obs_out) & 7) return RCBF_E_BAD_SHAPE;  // float2 row stores
+    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0,
+                                          stream, *prm, B, x, aux, step, episode, u_rl, mu, sigma, obs_out, u_out,
+                                          reward, cost, done, goal_met, status_out, fail_flag, auto_reset, seed,
+                                          env_offset));
+    return launch_status();
+}
+
+int rcbf_safe_rollout(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux, int32_t* step,
+                      uint32_t* episode, const float* u_rl, float* obs_out, float* reward_sum, float* cost_sum,
+                      int32_t* n_done, int32_t* fail_flag, uint64_t seed, int64_t env_offset, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0 || K < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0 || K == 0) return 0;
+    if (!x || !aux || !step || !u_rl || !reward_sum || !cost_sum || !n_done) return RCBF_E_NULL;
+    if (obs_out && (((uintptr_t)obs_out) & 7)) return RCBF_E_BAD_SHAPE;
+    RCBF_DISPATCH_MODE(prm, hipLaunchKernelGGL((k_safe_rollout<MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0,
+                                               stream, *prm, B, K, x, aux, step, episode, u_rl, obs_out, reward_sum,
+                                               cost_sum, n_done, fail_flag, seed, env_offset));
+    return launch_status();
+}
+
+}  // extern "C"

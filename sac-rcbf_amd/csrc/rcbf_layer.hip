@@ -1,0 +1,316 @@
+// rcbf_layer.hip -- CBFQPLayer kernels + C-ABI (include/rcbf_hip.h):
+// rcbf_build, rcbf_build_f64, rcbf_safe_action, rcbf_safe_action_backward.
+// One env per lane; the env's rows, QP iterate and active set stay in VGPRs.
+#include "rcbf_common.hpp"
+
+using namespace rcbf;
+
+namespace {
+
+template <int MODE, int K>
+__global__ void __launch_bounds__(kBlock) k_build(rcbf_params prm, int64_t B, const float* __restrict__ x,
+                                                  const float* __restrict__ u, const float* __restrict__ mu,
+                                                  const float* __restrict__ sigma, float* __restrict__ P_out,
+                                                  float* __restrict__ q_out, float* __restrict__ G_out,
+                                                  float* __restrict__ h_out) {
+    using D = Dims<MODE, K>;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    float xs[D::NS], us[D::NU], m[D::NS], s[D::NS];
+#pragma unroll
+    for (int k = 0; k < D::NS; ++k) {
+        xs[k] = x[i * D::NS + k];
+        m[k] = mu ? mu[i * D::NS + k] : 0.0f;
+        s[k] = sigma ? sigma[i * D::NS + k] : prior_sigma<MODE>(k);
+    }
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) us[c] = u[i * D::NU + c];
+    float G[D::M][D::N], h[D::M];
+    diff_rows<MODE, K>(prm, xs, us, m, s, G, h);
+#pragma unroll
+    for (int r = 0; r < D::M; ++r) {
+        h_out[i * D::M + r] = h[r];
+#pragma unroll
+        for (int k = 0; k < D::N; ++k) G_out[(i * D::M + r) * D::N + k] = G[r][k];
+    }
+    if (P_out) {
+        double pd[D::N];
+        diff_P<MODE>(pd);
+#pragma unroll
+        for (int a = 0; a < D::N; ++a)
+#pragma unroll
+            for (int b = 0; b < D::N; ++b) P_out[(i * D::N + a) * D::N + b] = (a == b) ? (float)pd[a] : 0.0f;
+    }
+    if (q_out) {
+#pragma unroll
+        for (int a = 0; a < D::N; ++a) q_out[i * D::N + a] = 0.0f;
+    }
+}
+
+template <int MODE, int K>
+__global__ void __launch_bounds__(kBlock) k_build_f64(rcbf_params prm, int64_t B, const double* __restrict__ x,
+                                                      const double* __restrict__ u, const double* __restrict__ mu,
+                                                      const double* __restrict__ sigma, double* __restrict__ P_out,
+                                                      double* __restrict__ q_out, double* __restrict__ G_out,
+                                                      double* __restrict__ h_out) {
+    using D = Dims<MODE, K>;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    double xs[D::NS], us[D::NU], m[D::NS], s[D::NS];
+#pragma unroll
+    for (int k = 0; k < D::NS; ++k) {
+        xs[k] = x[i * D::NS + k];
+        m[k] = mu ? mu[i * D::NS + k] : 0.0;
+        s[k] = sigma ? sigma[i * D::NS + k] : (double)prior_sigma<MODE>(k);
+    }
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) us[c] = u[i * D::NU + c];
+    double G[D::M][D::N], h[D::M];
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS)
+        cars_rows_cascade(prm, xs, us[0], G, h);
+    else
+        uni_rows_cascade<K>(prm, xs, us, m, s, G, h);
+#pragma unroll
+    for (int r = 0; r < D::M; ++r) {
+        h_out[i * D::M + r] = h[r];
+#pragma unroll
+        for (int k = 0; k < D::N; ++k) G_out[(i * D::M + r) * D::N + k] = G[r][k];
+    }
+    double pd[D::N];
+    cascade_P<MODE>(pd);
+    if (P_out) {
+#pragma unroll
+        for (int a = 0; a < D::N; ++a)
+#pragma unroll
+            for (int b = 0; b < D::N; ++b) P_out[(i * D::N + a) * D::N + b] = (a == b) ? pd[a] : 0.0;
+    }
+    if (q_out) {
+#pragma unroll
+        for (int a = 0; a < D::N; ++a) q_out[i * D::N + a] = 0.0;
+    }
+}
+
+template <int MODE, int K>
+__device__ __forceinline__ void load_layer_inputs(int64_t i, const float* x, const float* u, const float* mu,
+                                                  const float* sigma, float* xs, float* us, float* m, float* s) {
+    using D = Dims<MODE, K>;
+#pragma unroll
+    for (int k = 0; k < D::NS; ++k) {
+        xs[k] = x[i * D::NS + k];
+        m[k] = mu ? mu[i * D::NS + k] : 0.0f;
+        s[k] = sigma ? sigma[i * D::NS + k] : prior_sigma<MODE>(k);
+    }
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) us[c] = u[i * D::NU + c];
+}
+
+template <int SOLVER, int MODE, int K>
+__global__ void __launch_bounds__(kBlock) k_safe_action(rcbf_params prm, int64_t B, const float* __restrict__ x,
+                                                        const float* __restrict__ u, const float* __restrict__ mu,
+                                                        const float* __restrict__ sigma, float* __restrict__ u_out,
+                                                        int32_t* __restrict__ status_out, int32_t* fail_flag) {
+    using D = Dims<MODE, K>;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    float xs[D::NS], us[D::NU], m[D::NS], s[D::NS], uf[D::NU];
+    load_layer_inputs<MODE, K>(i, x, u, mu, sigma, xs, us, m, s);
+    LayerState<MODE, K> L;
+    layer_forward<SOLVER, MODE, K>(prm, xs, us, m, s, uf, L);
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) u_out[i * D::NU + c] = uf[c];
+    report(L.qp.status, status_out, i, fail_flag);
+}
+
+// d(final)/d(u_rl) on the active set of the exact optimum: the implicit-KKT
+// derivative qpth's QPFunction.backward approximates (D = lam/s over all
+// rows), through the row normaliser (torch.max routes dN to its argmax, the h
+// entry or a G entry that does not depend on u) and the clamp (torch.clamp
+// backward passes where lo <= v <= hi).  dh_r/du_c is closed form:
+//   CBF rows: dh/du = Lg (cars) or a_j (unicycle) = -G_raw[r][c];
+//   actuator rows (u_max - u, -u_min + u): -1 / +1.
+template <int SOLVER, int MODE, int K>
+__global__ void __launch_bounds__(kBlock) k_safe_action_bwd(rcbf_params prm, int64_t B, const float* __restrict__ x,
+                                                            const float* __restrict__ u, const float* __restrict__ mu,
+                                                            const float* __restrict__ sigma,
+                                                            const float* __restrict__ grad_u,
+                                                            float* __restrict__ grad_u_rl) {
+    using D = Dims<MODE, K>;
+    constexpr int N = D::N, M = D::M, NU = D::NU;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    float xs[D::NS], us[NU], m[D::NS], s[D::NS], uf[NU];
+    load_layer_inputs<MODE, K>(i, x, u, mu, sigma, xs, us, m, s);
+    LayerState<MODE, K> L;
+    layer_forward<SOLVER, MODE, K>(prm, xs, us, m, s, uf, L);
+    double pd[N];
+    diff_P<MODE>(pd);
+    // active rows (slots) of the solution
+    double GA[N][N];
+    int aidx[N];
+    int nact = 0;
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) {
+        aidx[sl] = -1;
+#pragma unroll
+        for (int k = 0; k < N; ++k) GA[sl][k] = 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        bool a = ((L.qp.active >> r) & 1u) && (nact < N);
+#pragma unroll
+        for (int sl = 0; sl < N; ++sl) {
+            bool here = a && (sl == nact);
+#pragma unroll
+            for (int k = 0; k < N; ++k) GA[sl][k] = here ? (double)L.G[r][k] : GA[sl][k];
+            aidx[sl] = here ? r : aidx[sl];
+        }
+        nact += a ? 1 : 0;
+    }
+    double J[NU][NU];  // J[a][c] = d(u_a + z_a)/d u_c
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        double dGn[M][N], dhn[M];
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            double dh;
+            constexpr int K0 = M - 2 * NU;  // first actuator row
+            if (r < K0) {
+                dh = -(double)L.Graw[r][c];
+            } else {
+                int col = (r - K0) / 2;
+                bool upper = ((r - K0) % 2) == 0;
+                dh = (col == c) ? (upper ? -1.0 : 1.0) : 0.0;
+            }
+            double hr = (double)L.hraw[r];
+            double dN = L.ish[r] ? ((hr > 0.0) ? dh : ((hr < 0.0) ? -dh : 0.0)) : 0.0;
+            double Nr = (double)L.Nrm[r];
+            dhn[r] = (dh - (double)L.h[r] * dN) / Nr;
+#pragma unroll
+            for (int k = 0; k < N; ++k) dGn[r][k] = -(double)L.G[r][k] * (dN / Nr);
+        }
+        // P dz + dGn' lam + G_A' dlam = 0 ;  G_A dz = dhn_A - dGn_A z
+        double rhs1[N], rhs2[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            double acc = 0.0;
+#pragma unroll
+            for (int r = 0; r < M; ++r) acc -= dGn[r][k] * L.qp.lam[r];
+            rhs1[k] = acc;
+        }
+#pragma unroll
+        for (int sl = 0; sl < N; ++sl) {
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < M; ++r) {
+                if (r == aidx[sl]) {
+                    double acc = dhn[r];
+#pragma unroll
+                    for (int k = 0; k < N; ++k) acc -= dGn[r][k] * L.qp.z[k];
+                    v = acc;
+                }
+            }
+            rhs2[sl] = (sl < nact) ? v : 0.0;
+        }
+        double dz[N];
+        if (nact == N) {  // vertex: dz = G_A^-1 rhs2
+            double A[N][N], b[N];
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                b[a] = rhs2[a];
+#pragma unroll
+                for (int k = 0; k < N; ++k) A[a][k] = GA[a][k];
+            }
+            gauss_solve<N>(A, b, dz);
+        } else {  // dlam = S^-1 (G_A P^-1 rhs1 - rhs2), dz = P^-1 (rhs1 - G_A' dlam)
+            double PG[N][N], Pr1[N], S[N][N], w[N], dl[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) Pr1[k] = rhs1[k] / pd[k];
+#pragma unroll
+            for (int sl = 0; sl < N; ++sl)
+#pragma unroll
+                for (int k = 0; k < N; ++k) PG[sl][k] = GA[sl][k] / pd[k];
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+#pragma unroll
+                for (int b = 0; b < N; ++b) {
+                    bool in = (a < nact) && (b < nact);
+                    S[a][b] = in ? dotd<N>(GA[a], PG[b]) : (a == b ? 1.0 : 0.0);
+                }
+                w[a] = (a < nact) ? dotd<N>(GA[a], Pr1) - rhs2[a] : 0.0;
+            }
+            ldl_solve<N>(S, w, dl);
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                double acc = rhs1[k];
+#pragma unroll
+                for (int sl = 0; sl < N; ++sl) acc -= GA[sl][k] * ((sl < nact) ? dl[sl] : 0.0);
+                dz[k] = acc / pd[k];
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) J[a][c] = (a == c ? 1.0 : 0.0) + dz[a];
+    }
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        double acc = 0.0;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            float v = us[a] + (float)L.qp.z[a];
+            bool pass = (v >= (float)prm.u_min[a]) && (v <= (float)prm.u_max[a]);
+            acc += pass ? (double)grad_u[i * NU + a] * J[a][c] : 0.0;
+        }
+        grad_u_rl[i * NU + c] = (float)acc;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rcbf_build(const rcbf_params* prm, int64_t B, const float* x, const float* u_rl, const float* mu,
+               const float* sigma, float* P_out, float* q_out, float* G_out, float* h_out, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !u_rl || !G_out || !h_out) return RCBF_E_NULL;
+    RCBF_DISPATCH_MODE(prm, hipLaunchKernelGGL((k_build<MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0, stream,
+                                               *prm, B, x, u_rl, mu, sigma, P_out, q_out, G_out, h_out));
+    return launch_status();
+}
+
+int rcbf_build_f64(const rcbf_params* prm, int64_t B, const double* x, const double* u_nom, const double* mu,
+                   const double* sigma, double* P_out, double* q_out, double* G_out, double* h_out,
+                   hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !u_nom || !G_out || !h_out) return RCBF_E_NULL;
+    RCBF_DISPATCH_MODE(prm, hipLaunchKernelGGL((k_build_f64<MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0,
+                                               stream, *prm, B, x, u_nom, mu, sigma, P_out, q_out, G_out, h_out));
+    return launch_status();
+}
+
+int rcbf_safe_action(const rcbf_params* prm, int64_t B, const float* x, const float* u_rl, const float* mu,
+                     const float* sigma, float* u_out, int32_t* status_out, int32_t* fail_flag, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !u_rl || !u_out) return RCBF_E_NULL;
+    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_action<SOLVER_, MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0,
+                                          stream, *prm, B, x, u_rl, mu, sigma, u_out, status_out, fail_flag));
+    return launch_status();
+}
+
+int rcbf_safe_action_backward(const rcbf_params* prm, int64_t B, const float* x, const float* u_rl,
+                              const float* mu, const float* sigma, const float* grad_u, float* grad_u_rl,
+                              hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !u_rl || !grad_u || !grad_u_rl) return RCBF_E_NULL;
+    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_action_bwd<SOLVER_, MODE_, K_>), dim3(grid_for(B)), dim3(kBlock),
+                                          0, stream, *prm, B, x, u_rl, mu, sigma, grad_u, grad_u_rl));
+    return launch_status();
+}
+
+}  // extern "C"

@@ -9,11 +9,13 @@
   dynamics_mode, kp/k_brake, hazards_*) on a B = 1 device env, so the
   reference's main.py loop runs unchanged.
 
-Per-env state: x (B, n_s) f64 = env.state; aux (B,) f64 = env.t (cars) or
-env.last_goal_dist (unicycle); step (B,) i32 = env.episode_step; episode
-(B,) i32 = reset counter keying the counter-based reset RNG (so the cars'
-N(0, 0.5) reset draw depends only on (seed, global env index, episode) and is
-identical however the envs are sharded over GPUs).
+Per-env state in HBM, component-major (SoA) so every component access of a
+wavefront is contiguous: x (n_s, B) f64 = env.state (`.state` is the (B, n_s)
+view); aux (B,) f64 = env.t (cars) or env.last_goal_dist (unicycle); step (B,)
+i32 = env.episode_step; episode (B,) i32 = reset counter keying the
+counter-based reset RNG (so the cars' N(0, 0.5) reset draw depends only on
+(seed, global env index, episode) and is identical however the envs are
+sharded over GPUs).
 """
 import ctypes
 
@@ -103,7 +105,7 @@ class BatchedEnv:
         self.seed_value = int(seed)
         self.env_offset = int(env_offset)  # global index of env 0 (sharding)
         B, d = self.num_envs, self.device
-        self.x = torch.zeros(B, self.n_s, dtype=torch.float64, device=d)
+        self.x = torch.zeros(self.n_s, B, dtype=torch.float64, device=d)  # SoA
         self.aux = torch.zeros(B, dtype=torch.float64, device=d)
         self.step_count = torch.zeros(B, dtype=torch.int32, device=d)
         self.episode = torch.zeros(B, dtype=torch.int32, device=d)
@@ -112,6 +114,23 @@ class BatchedEnv:
         self.fail_flag = torch.zeros(1, dtype=torch.int32, device=d)
         _lib.load()
         self.reset()
+
+    @property
+    def state(self):
+        """(B, n_s) view of the SoA state."""
+        return self.x.t()
+
+    def state_numpy(self):
+        return self.x.t().cpu().numpy()
+
+    def load_state(self, x=None, aux=None, step=None):
+        """Overwrite the state of every env: x (B, n_s), aux (B,), step (B,)."""
+        if x is not None:
+            self.x.copy_(torch.as_tensor(np.asarray(x), dtype=torch.float64, device=self.device).t())
+        if aux is not None:
+            self.aux.copy_(torch.as_tensor(np.asarray(aux), dtype=torch.float64, device=self.device))
+        if step is not None:
+            self.step_count.copy_(torch.as_tensor(np.asarray(step), dtype=torch.int32, device=self.device))
 
     def _rng_seed(self):
         return self.seed_value & 0xFFFFFFFFFFFFFFFF
@@ -236,11 +255,11 @@ class _SingleEnv(_EnvBase):
     # env.state / env.t / env.episode_step / env.last_goal_dist as numpy views
     @property
     def state(self):
-        return self._b.x[0].cpu().numpy().copy()
+        return self._b.x[:, 0].cpu().numpy().copy()
 
     @state.setter
     def state(self, v):
-        self._b.x[0] = torch.as_tensor(np.asarray(v, np.float64), device=self._b.device)
+        self._b.x[:, 0] = torch.as_tensor(np.asarray(v, np.float64), device=self._b.device)
 
     @property
     def episode_step(self):

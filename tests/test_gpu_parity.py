@@ -46,7 +46,7 @@ def _layer(env, gamma_b, solver=0):
 # ----------------------------------------------------------------------------
 # CBFQPLayer vs reference fixtures
 # ----------------------------------------------------------------------------
-@pytest.mark.parametrize("solver", [0, 1])
+@pytest.mark.parametrize("solver", [0, 1, 2])
 @pytest.mark.parametrize("tag", ["prior", "rand"])
 def test_cars_layer_golden(golden, tag, solver):
     d = golden("cars_layer")
@@ -146,10 +146,10 @@ def test_cars_env_traj(golden):
     E = d["cars_noise"].shape[0]
     env = BatchedSimulatedCarsEnv(E)
     env.reset(noise=d["cars_noise"])
-    assert np.array_equal(env.x.cpu().numpy(), d["cars_state"][:, 0])
+    assert np.array_equal(env.state_numpy(), d["cars_state"][:, 0])
     for k in range(300):
         obs, r, done, info = env.step(dev(d["cars_actions"][:, k]), auto_reset=False, obs64=True)
-        assert rel(env.x.cpu().numpy(), d["cars_state"][:, k + 1]) <= 1e-12
+        assert rel(env.state_numpy(), d["cars_state"][:, k + 1]) <= 1e-12
         assert rel(info["obs64"].cpu().numpy(), d["cars_obs"][:, k + 1]) <= 1e-12
         rr = r.cpu().numpy()
         assert np.all(np.abs(rr - d["cars_reward"][:, k]) <= 2 * np.spacing(np.abs(rr).astype(np.float32)))
@@ -164,20 +164,18 @@ def test_unicycle_env_traj(golden):
     env = BatchedUnicycleEnv(1)
     for k in range(1000):
         obs, r, done, info = env.step(dev(d["uni_actions"][k][None]), auto_reset=False, obs64=True)
-        assert rel(env.x.cpu().numpy()[0], d["uni_state"][k + 1]) <= 1e-12
+        assert rel(env.state_numpy()[0], d["uni_state"][k + 1]) <= 1e-12
         assert rel(info["obs64"].cpu().numpy()[0], d["uni_obs"][k + 1]) <= 1e-12
         assert abs(r.item() - d["uni_reward"][k]) <= 1e-12
         assert info["cost"].item() == d["uni_cost"][k] and bool(done.item()) == bool(d["uni_done"][k])
     # random starts: hazard contacts, goal hits, time limit
     E, T = d["unir_x0"].shape[0], d["unir_actions"].shape[1]
     env = BatchedUnicycleEnv(E)
-    env.x.copy_(dev(d["unir_x0"], torch.float64))
-    env.aux.copy_(dev(d["unir_lastdist"][:, 0], torch.float64))
-    env.step_count.copy_(dev(d["unir_step0"], torch.int32))
+    env.load_state(d["unir_x0"], d["unir_lastdist"][:, 0], d["unir_step0"])
     alive = np.ones(E, bool)
     for k in range(T):
         obs, r, done, info = env.step(dev(d["unir_actions"][:, k]), auto_reset=False, obs64=True)
-        xs = env.x.cpu().numpy()
+        xs = env.state_numpy()
         assert rel(xs[alive], d["unir_state"][alive, k + 1]) <= 1e-11
         assert np.array_equal(info["cost"].cpu().numpy()[alive], d["unir_cost"][alive, k])
         assert np.array_equal(done.cpu().numpy()[alive], d["unir_done"][alive, k])
@@ -249,13 +247,13 @@ def _cars_states(B, seed):
     return x, t, st
 
 
-@pytest.mark.parametrize("solver", [0, 1])
+@pytest.mark.parametrize("solver", [0, 1, 2])
 def test_fused_safe_step_cars(solver):
     from rcbf_amd.envs import BatchedSimulatedCarsEnv
     B = 4096
     x, t, st = _cars_states(B, 5)
     env = BatchedSimulatedCarsEnv(B)
-    env.x.copy_(dev(x, torch.float64)); env.aux.copy_(dev(t, torch.float64)); env.step_count.copy_(dev(st, torch.int32))
+    env.load_state(x, t, st)
     layer = _layer(env, 20.0, solver)
     rng = np.random.default_rng(6)
     for k in range(3):
@@ -266,7 +264,7 @@ def test_fused_safe_step_cars(solver):
         fin, aux = O.safe_action_diff("SimulatedCars", s32, u, mu.astype(np.float32), sg.astype(np.float32), 20.0)
         assert rel(out["u"].cpu().numpy(), fin) <= 1e-4
         x, t, st, o, r, c, dn = O.cars_step(x, t, st, fin)
-        assert rel(env.x.cpu().numpy(), x) <= 1e-9
+        assert rel(env.state_numpy(), x) <= 1e-9
         assert rel(obs.cpu().numpy(), o.astype(np.float32)) <= 1e-6
         assert rel(rew.cpu().numpy(), r) <= 1e-6
         assert np.array_equal(out["cost"].cpu().numpy(), c.astype(np.float32))
@@ -283,7 +281,7 @@ def test_fused_safe_step_unicycle(k):
     env = BatchedUnicycleEnv(B, hazards_locations=hz)
     x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
     ld = O.uni_goal_dist(x); st = np.zeros(B, np.int64)
-    env.x.copy_(dev(x, torch.float64)); env.aux.copy_(dev(ld, torch.float64)); env.step_count.zero_()
+    env.load_state(x, ld, np.zeros(B))
     layer = _layer(env, 20.0)
     for it in range(3):
         u = rng.uniform(-1, 1, (B, 2)).astype(np.float32)
@@ -293,7 +291,7 @@ def test_fused_safe_step_unicycle(k):
                                       np.full((B, 3), 0.2, np.float32), 20.0, hazards=hz)
         assert rel(out["u"].cpu().numpy(), fin) <= 1e-4
         x, ld, st, o, r, c, dn, gm = O.uni_step(x, ld, st, fin, hazards=hz)
-        assert rel(env.x.cpu().numpy(), x) <= 1e-9
+        assert rel(env.state_numpy(), x) <= 1e-9
         assert rel(rew.cpu().numpy(), r) <= 1e-5
     env.check_failures()
 
@@ -323,7 +321,7 @@ def test_auto_reset_and_rng_sharding_invariance():
     full = BatchedSimulatedCarsEnv(B, seed=9)
     lo = BatchedSimulatedCarsEnv(B // 2, seed=9, env_offset=0)
     hi = BatchedSimulatedCarsEnv(B // 2, seed=9, env_offset=B // 2)
-    assert torch.equal(full.x[:B // 2], lo.x) and torch.equal(full.x[B // 2:], hi.x)
+    assert torch.equal(full.state[:B // 2], lo.state) and torch.equal(full.state[B // 2:], hi.state)
     lf = _layer(full, 20.0)
     u = torch.zeros(B, 1, device="cuda")
     nd = 0
@@ -331,7 +329,7 @@ def test_auto_reset_and_rng_sharding_invariance():
         _, _, d, _ = full.safe_step(u, lf)
         nd += int(d.sum().item()) if k == 299 else 0
     assert nd == B and int(full.step_count.max().item()) == 0 and int(full.episode.min().item()) == 2
-    v = full.x[:, 1].cpu().numpy() - 30.0
+    v = full.state[:, 1].cpu().numpy() - 30.0
     assert 0.3 < v.std() < 0.7  # N(0, 0.5) reset draw
 
 
