@@ -23,7 +23,85 @@ constexpr int kBlock = RCBF_BLOCK;
 #endif
 constexpr int kAblate = RCBF_ABLATE;
 
+// Envs per 64-lane wavefront in the env kernels (performance study knob:
+// 32 leaves the upper half of every wave idle and doubles the wave count).
+#ifndef RCBF_ENVS_PER_WAVE
+#define RCBF_ENVS_PER_WAVE 64
+#endif
+constexpr int kEnvsPerWave = RCBF_ENVS_PER_WAVE;
+constexpr int kEnvsPerBlock = kBlock / 64 * kEnvsPerWave;
+
 inline unsigned grid_for(int64_t B) { return (unsigned)((B + kBlock - 1) / kBlock); }
+inline unsigned grid_for_envs(int64_t B) { return (unsigned)((B + kEnvsPerBlock - 1) / kEnvsPerBlock); }
+
+// env index of this lane in the env kernels; -1 for an idle lane
+__device__ __forceinline__ int64_t env_index() {
+    if constexpr (kEnvsPerWave == 64) {
+        return (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    } else {
+        int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane >= kEnvsPerWave) return -1;
+        return (int64_t)blockIdx.x * kEnvsPerBlock + wave * kEnvsPerWave + lane;
+    }
+}
+
+// Output store flavour of the env kernels (performance study knob):
+//   0 = plain stores (lines stay dirty in the XCD's L2 until the kernel-end
+//       write-back), 1 = write-through `sc1` stores (agent-scope relaxed
+//       atomic stores: the line leaves L2 as it is written), 2 = `nt` stores.
+#ifndef RCBF_STORE_MODE
+#define RCBF_STORE_MODE 0
+#endif
+constexpr int kStoreMode = RCBF_STORE_MODE;
+
+template <typename T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+    if constexpr (kStoreMode == 1) {
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (kStoreMode == 2) {
+        __builtin_nontemporal_store(v, p);
+    } else {
+        *p = v;
+    }
+}
+
+// 8-byte pair store (obs rows): one dwordx2 store in every flavour
+__device__ __forceinline__ void st_out2(float* p, float a, float b) {
+    if constexpr (kStoreMode == 0) {
+        *reinterpret_cast<float2*>(p) = make_float2(a, b);
+    } else {
+        union {
+            float f[2];
+            uint64_t u;
+        } w;
+        w.f[0] = a;
+        w.f[1] = b;
+        st_out<uint64_t>(reinterpret_cast<uint64_t*>(p), w.u);
+    }
+}
+
+// Diagnostic build only (-DRCBF_STAMPS=1): lane 0 of every wave records
+// s_memtime at phase boundaries of the fused step into the status_out buffer
+// reinterpreted as uint64 [wave][16].  Never part of the product build.
+#ifndef RCBF_STAMPS
+#define RCBF_STAMPS 0
+#endif
+#if RCBF_STAMPS
+#define RCBF_STAMP(buf, j, drain)                                                          \
+    do {                                                                                   \
+        if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                       \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        unsigned long long t_;                                                             \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        if ((threadIdx.x & 63) == 0 && (buf))                                              \
+            (buf)[((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + (j)] = t_; \
+    } while (0)
+#else
+#define RCBF_STAMP(buf, j, drain) \
+    do {                          \
+    } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // mode traits
@@ -99,10 +177,12 @@ struct LayerState {
 
 // CBFQPLayer.get_safe_action for one env (diff_cbf_qp.py:44-79):
 // build -> normalise -> fp64 QP -> .float() -> clamp.
-template <int SOLVER, int MODE, int K>
+// NEED_LAM: the caller needs the multipliers and the active set (backward);
+// otherwise the cars path uses the 1-D exact solver (cars_qp_1d).
+template <int SOLVER, int MODE, int K, bool NEED_LAM = false>
 __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const float* xs, const float* u,
                                               const float* mu, const float* sig, float* u_final,
-                                              LayerState<MODE, K>& L) {
+                                              LayerState<MODE, K>& L, unsigned long long* stamps = nullptr) {
     using D = Dims<MODE, K>;
     if constexpr ((kAblate & 2) != 0) {
 #pragma unroll
@@ -118,6 +198,7 @@ __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const floa
         for (int k = 0; k < D::N; ++k) L.Graw[r][k] = L.G[r][k];
     }
     normalize_rows<D::N, D::M, float>(L.G, L.h, L.Nrm, L.ish);
+    RCBF_STAMP(stamps, 3, false);
     PMat<D::N, true> pm;
     double pd[D::N], q[D::N];
     diff_P<MODE>(pd);
@@ -128,9 +209,12 @@ __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const floa
 #pragma unroll
         for (int k = 0; k < D::N; ++k) L.qp.z[k] = 1e-30 * (double)(L.G[0][k] + L.h[k % D::M]);
         L.qp.status = RCBF_QP_OK;
+    } else if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && SOLVER == RCBF_SOLVER_ACTIVE_SET && !NEED_LAM) {
+        cars_qp_1d<float>(pm, L.G, L.h, L.qp.z, L.qp.status);
     } else {
         qp_solve<SOLVER, D::N, D::M, true, float>(pm, q, L.G, L.h, prm.max_iter, prm.eps, L.qp);
     }
+    RCBF_STAMP(stamps, 4, false);
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) {
         float v = u[c] + (float)L.qp.z[c];
@@ -198,13 +282,22 @@ template <int SOLVER, int MODE, int K>
 __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i, double* xs, double& a, int& st,
                                               uint32_t* episode, const float* us, const float* m, const float* s,
                                               float* uf, float& rew, float& cst, bool& dn, bool& gm, int& status,
-                                              int auto_reset, uint64_t seed, int64_t off) {
+                                              int auto_reset, uint64_t seed, int64_t off,
+                                              unsigned long long* stamps = nullptr) {
     using D = Dims<MODE, K>;
     float s32[D::NS];
     state_from_env<MODE>(xs, s32);
+    RCBF_STAMP(stamps, 2, false);
     LayerState<MODE, K> L;
-    layer_forward<SOLVER, MODE, K>(prm, s32, us, m, s, uf, L);
+    layer_forward<SOLVER, MODE, K>(prm, s32, us, m, s, uf, L, stamps);
     status = L.qp.status;
+#if RCBF_STAMPS
+    {
+        unsigned long long fb = __ballot(L.qp.iters == 1);
+        if ((threadIdx.x & 63) == 0 && stamps)
+            stamps[((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + 9] = __popcll(fb);
+    }
+#endif
     if constexpr ((kAblate & 4) != 0) {
 #pragma unroll
         for (int k = 0; k < D::NS; ++k) xs[k] += 1e-3 * (double)uf[0];
@@ -228,6 +321,7 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
         dn = o.done;
         gm = o.goal;
     }
+    RCBF_STAMP(stamps, 5, false);
     if (auto_reset && dn) {
         uint32_t ep = episode ? episode[i] + 1u : 0u;
         if (episode) episode[i] = ep;

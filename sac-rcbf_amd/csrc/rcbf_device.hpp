@@ -114,6 +114,43 @@ __device__ __forceinline__ void gauss_solve(double A[N][N], double* b, double* x
     }
 }
 
+// fp64 reciprocal: v_rcp_f64 + two Newton steps (error ~1 ulp), no
+// div_scale/div_fixup chain.  rcp64(0) = inf.
+__device__ __forceinline__ double rcp64(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    return (d == 0.0) ? __builtin_copysign(__builtin_huge_val(), d) : r;
+}
+
+// fp32 a / b, correctly rounded, via one fp64 reciprocal of b: the fp64
+// product a * rcp64(b) is within ~2^-52 (relative) of a/b, while a quotient
+// of two 24-bit significands is never within 2^-48 of an fp32 rounding
+// midpoint, so rounding it to fp32 gives RN32(a/b) -- bit-identical to the
+// IEEE division torch performs.  Lets a row share one reciprocal.
+__device__ __forceinline__ float div_f32_via_rcp(float a, double rb) { return (float)((double)a * rb); }
+
+// sin(x) for |x| <= 1.3 by its Taylor series to x^21 (truncation < 2e-19,
+// ~1 ulp rounding), else the library sin.  The cars lead-car term
+// sin(0.2 t) stays below 1.3 for t <= 6.5 s, i.e. within one 300-step episode.
+__device__ __forceinline__ double sin_small(double x) {
+    if (!(fabs(x) <= 1.3)) return sin(x);
+    const double x2 = x * x;
+    double p = -1.9572941063391263e-20;  // -1/21!
+    p = fma(p, x2, 8.2206352466243297e-18);   // 1/19!
+    p = fma(p, x2, -2.8114572543455206e-15);  // -1/17!
+    p = fma(p, x2, 7.6471637318198164e-13);   // 1/15!
+    p = fma(p, x2, -1.6059043836821613e-10);  // -1/13!
+    p = fma(p, x2, 2.5052108385441720e-08);   // 1/11!
+    p = fma(p, x2, -2.7557319223985893e-06);  // -1/9!
+    p = fma(p, x2, 1.9841269841269841e-04);   // 1/7!
+    p = fma(p, x2, -8.3333333333333332e-03);  // -1/5!
+    p = fma(p, x2, 1.6666666666666666e-01);   // 1/3!  (sign applied below)
+    return fma(-x * x2, p, x);
+}
+
 // ---------------------------------------------------------------------------
 // Strictly convex QP   min 1/2 z'Pz + q'z   s.t.  G z <= h
 // P is given by its inverse (diagonal or full, n <= 3).
@@ -835,6 +872,166 @@ __device__ __forceinline__ void enum2_solve(const PMat<2, true>& pm, const R (*G
     out.status = !finite ? RCBF_QP_NONFINITE : (okz ? RCBF_QP_OK : RCBF_QP_INFEASIBLE);
 }
 
+// Fast exact solver for n = 2: the candidate selection of enum2_solve runs in
+// fp32 (twice the fp64 rate, cheap approximate reciprocals), then the chosen
+// active set is re-solved in fp64 and its KKT conditions are verified in fp64
+// (primal feasibility of every row, non-negative multipliers).  A verified KKT
+// point IS the unique optimum, so the result equals enum2_solve's; when the
+// certificate fails (fp32 picked a near-tie wrongly) the lane falls back to
+// the fp64 enumeration.
+template <int M, typename R>
+__device__ __forceinline__ void enum2_solve_fast(const PMat<2, true>& pm, const R (*G)[2], const R* h,
+                                                 QPResult<2, M>& out) {
+    const float pi0 = (float)pm.Pinv[0][0], pi1 = (float)pm.Pinv[1][1];
+    const float p0 = (float)pm.P[0][0], p1 = (float)pm.P[1][1];
+    float g0[M], g1[M], hh[M];
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        g0[r] = (float)G[r][0];
+        g1[r] = (float)G[r][1];
+        hh[r] = (float)h[r];
+    }
+    float best = __builtin_huge_valf();
+    uint32_t bact = 0;
+    auto consider = [&](float z0, float z1, uint32_t act, bool valid) {
+        bool feas = valid;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            float v = fmaf(g0[r], z0, fmaf(g1[r], z1, -hh[r]));
+            feas = feas && (v <= 1e-5f * (1.0f + fabsf(hh[r])));
+        }
+        float obj = fmaf(p0 * z0, z0, p1 * z1 * z1);
+        bool take = feas && (obj < best);
+        best = take ? obj : best;
+        bact = take ? act : bact;
+    };
+    consider(0.0f, 0.0f, 0u, true);
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        float nrm = fmaf(g0[r] * pi0, g0[r], g1[r] * pi1 * g1[r]);
+        bool ok = nrm > 1e-30f;
+        float f = hh[r] * __builtin_amdgcn_rcpf(ok ? nrm : 1.0f);
+        consider(pi0 * g0[r] * f, pi1 * g1[r] * f, 1u << r, ok);
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+#pragma unroll
+        for (int s = r + 1; s < M; ++s) {
+            float det = fmaf(g0[r], g1[s], -g1[r] * g0[s]);
+            bool ok = fabsf(det) > 1e-7f;
+            float inv = __builtin_amdgcn_rcpf(ok ? det : 1.0f);
+            float z0 = fmaf(hh[r], g1[s], -hh[s] * g1[r]) * inv;
+            float z1 = fmaf(g0[r], hh[s], -g0[s] * hh[r]) * inv;
+            consider(z0, z1, (1u << r) | (1u << s), ok);
+        }
+    }
+    // fp64 re-solve of the chosen set and its KKT certificate
+    int ra = -1, rb = -1;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        bool a = (bact >> r) & 1u;
+        rb = (a && ra >= 0 && rb < 0) ? r : rb;
+        ra = (a && ra < 0) ? r : ra;
+    }
+    double ga0 = 0, ga1 = 0, gb0 = 0, gb1 = 0, ha = 0, hb = 0;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        ga0 = (r == ra) ? (double)G[r][0] : ga0;
+        ga1 = (r == ra) ? (double)G[r][1] : ga1;
+        ha = (r == ra) ? (double)h[r] : ha;
+        gb0 = (r == rb) ? (double)G[r][0] : gb0;
+        gb1 = (r == rb) ? (double)G[r][1] : gb1;
+        hb = (r == rb) ? (double)h[r] : hb;
+    }
+    const double dpi0 = pm.Pinv[0][0], dpi1 = pm.Pinv[1][1], dp0 = pm.P[0][0], dp1 = pm.P[1][1];
+    double z0 = 0.0, z1 = 0.0, la = 0.0, lb = 0.0;
+    if (rb >= 0) {
+        double det = ga0 * gb1 - ga1 * gb0;
+        double inv = 1.0 / det;
+        z0 = (ha * gb1 - hb * ga1) * inv;
+        z1 = (ga0 * hb - gb0 * ha) * inv;
+        double Pz0 = dp0 * z0, Pz1 = dp1 * z1;
+        la = (-Pz0 * gb1 + Pz1 * gb0) * inv;
+        lb = (-ga0 * Pz1 + ga1 * Pz0) * inv;
+    } else if (ra >= 0) {
+        double nrm = fma(ga0 * dpi0, ga0, ga1 * dpi1 * ga1);
+        double f = ha / nrm;
+        z0 = dpi0 * ga0 * f;
+        z1 = dpi1 * ga1 * f;
+        la = -f;
+    }
+    bool cert = isfinite(z0) && isfinite(z1) && (la >= -1e-12) && (lb >= -1e-12);
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        double v = fma((double)G[r][0], z0, fma((double)G[r][1], z1, -(double)h[r]));
+        cert = cert && (v <= 1e-9 * (1.0 + fabs((double)h[r])));
+    }
+    if (!cert) {  // rare: near-tie mis-selected in fp32 (or non-finite input)
+        enum2_solve<M, R>(pm, G, h, out);
+        return;
+    }
+    out.z[0] = z0;
+    out.z[1] = z1;
+#pragma unroll
+    for (int r = 0; r < M; ++r) out.lam[r] = (r == ra) ? la : ((r == rb) ? lb : 0.0);
+    out.active = bact;
+    out.nact = (ra >= 0) + (rb >= 0);
+    out.iters = 0;
+    out.status = RCBF_QP_OK;
+}
+
+// Exact solver for the CARS QP structure (both formulations):
+//   rows 0,1:  g_r0 u + g_r1 eps <= h_r  with g_r1 < 0 (the -200 slack column)
+//   row 2:     g_20 u <= h_2  (g_20 > 0)     row 3:  g_30 u <= h_3  (g_30 < 0)
+//   objective  1/2 (p0 u^2 + p1 eps^2)
+// For a fixed u the best slack is eps*(u) = max(0, e0(u), e1(u)) with the
+// affine e_r(u) = (h_r - g_r0 u) / g_r1, so the QP is the 1-D convex problem
+// min_{L <= u <= U} phi(u) = p0 u^2 + p1 eps*(u)^2, U = h2/g20, L = h3/g30.
+// phi is convex and piecewise quadratic; its unconstrained minimiser is 0
+// (eps* = 0 piece), a stationary point of one of the two e_r pieces, or the
+// kink e0 = e1 (phi is differentiable where an e_r crosses 0), and the
+// constrained minimiser is that point clamped to [L, U].  Evaluating phi
+// exactly at the four clamped candidates and keeping the smallest is
+// therefore exact -- no feasibility or dual tests, no active-set loop, and
+// any extra candidate is harmless (all lie in [L, U]).  ~60 fp64 ops vs
+// ~400 for the generic enumeration.  Multipliers are not produced (the
+// forward does not need them; the backward uses enum2_solve).
+template <typename R>
+__device__ __forceinline__ void cars_qp_1d(const PMat<2, true>& pm, const R (*G)[2], const R* h, double* z,
+                                           int& status) {
+    const double p0 = pm.P[0][0], p1 = pm.P[1][1];
+    const double g00 = (double)G[0][0], g01 = (double)G[0][1], h0 = (double)h[0];
+    const double g10 = (double)G[1][0], g11 = (double)G[1][1], h1 = (double)h[1];
+    const double U = (double)h[2] * rcp64((double)G[2][0]);
+    const double L = (double)h[3] * rcp64((double)G[3][0]);
+    const double i0 = rcp64(g01), i1 = rcp64(g11);
+    const double a0 = -g00 * i0, b0 = h0 * i0;  // e0(u) = a0 u + b0
+    const double a1 = -g10 * i1, b1 = h1 * i1;  // e1(u) = a1 u + b1
+    const double c1 = -(p1 * a0 * b0) * rcp64(fma(p1 * a0, a0, p0));
+    const double c2 = -(p1 * a1 * b1) * rcp64(fma(p1 * a1, a1, p0));
+    const double den = a0 - a1;
+    const double c3 = (den != 0.0) ? (b1 - b0) * rcp64(den) : 0.0;
+    auto clampu = [&](double u) { return fmin(fmax(u, L), U); };
+    auto phi = [&](double u) {
+        double e = fmax(0.0, fmax(fma(a0, u, b0), fma(a1, u, b1)));
+        return fma(p0 * u, u, p1 * e * e);
+    };
+    double ub = clampu(0.0), fb = phi(ub);
+    double u1 = clampu(c1), f1 = phi(u1);
+    double u2 = clampu(c2), f2 = phi(u2);
+    double u3 = clampu(c3), f3 = phi(u3);
+    ub = (f1 < fb) ? u1 : ub;
+    fb = fmin(f1, fb);
+    ub = (f2 < fb) ? u2 : ub;
+    fb = fmin(f2, fb);
+    ub = (f3 < fb) ? u3 : ub;
+    z[0] = ub;
+    z[1] = fmax(0.0, fmax(fma(a0, ub, b0), fma(a1, ub, b1)));
+    bool ok = isfinite(z[0]) && isfinite(z[1]) && (L <= U);
+    status = ok ? RCBF_QP_OK : (isfinite(g00 + g01 + h0 + g10 + g11 + h1 + U + L) ? RCBF_QP_INFEASIBLE
+                                                                               : RCBF_QP_NONFINITE);
+}
+
 // Compile-time solver choice (the host dispatches on rcbf_params.solver):
 //   RCBF_SOLVER_ACTIVE_SET: exact -- KKT enumeration for n = 2, Goldfarb-Idnani
 //                           for n = 3 or a full P;
@@ -846,7 +1043,11 @@ __device__ __forceinline__ void qp_solve(const PMat<N, DIAG>& pm, const double* 
     if constexpr (SOLVER == RCBF_SOLVER_PDIPM) {
         pdipm_solve<N, M, DIAG, R>(pm, q, G, h, max_iter > 0 ? max_iter : 50, eps > 0 ? eps : 1e-10, out);
     } else if constexpr (SOLVER == RCBF_SOLVER_ACTIVE_SET && N == 2 && DIAG) {
+#if defined(RCBF_ENUM2_FP64_ONLY)
         enum2_solve<M, R>(pm, G, h, out);
+#else
+        enum2_solve_fast<M, R>(pm, G, h, out);
+#endif
     } else {
         gi_solve<N, M, DIAG, R>(pm, q, G, h, max_iter > 0 ? max_iter : 4 * (M + N) + 8, out);
     }
@@ -871,9 +1072,16 @@ __device__ __forceinline__ void normalize_rows(T (*G)[N], T* h, T* Nrm, bool* ar
         T nr = ish ? ah : mx;
         Nrm[r] = nr;
         if (argmax_is_h) argmax_is_h[r] = ish;
+        if constexpr (sizeof(T) == 4) {
+            const double rn = rcp64((double)nr);  // one reciprocal per row, exact fp32 quotients
 #pragma unroll
-        for (int k = 0; k < N; ++k) G[r][k] = G[r][k] / nr;
-        h[r] = h[r] / nr;
+            for (int k = 0; k < N; ++k) G[r][k] = div_f32_via_rcp(G[r][k], rn);
+            h[r] = div_f32_via_rcp(h[r], rn);
+        } else {
+#pragma unroll
+            for (int k = 0; k < N; ++k) G[r][k] = G[r][k] / nr;
+            h[r] = h[r] / nr;
+        }
     }
 }
 
@@ -1060,7 +1268,7 @@ __device__ __forceinline__ void cars_env_step(const rcbf_params& prm, double* xs
                                               CarsStepOut& o) {
 #pragma clang fp contract(off)
     const double kp = prm.kp, kb = prm.k_brake, dt = 0.02;
-    double vdes0 = 30.0 - 10.0 * sin(0.2 * t);
+    double vdes0 = 30.0 - 10.0 * sin_small(0.2 * t);
     double acc[5];
     acc[0] = kp * (vdes0 - xs[1]);
 #pragma unroll
@@ -1094,12 +1302,21 @@ __device__ __forceinline__ void cars_env_step(const rcbf_params& prm, double* xs
     o.cost = cost;
 }
 
+// x / d for a constant d, correctly rounded: q = RN(x * RN(1/d)) is within
+// 1 ulp of x/d, r = x - q*d is exact with one FMA, and q + r*RN(1/d) rounds
+// to RN(x/d) (Markstein's theorem).  3 FMA-pipe ops instead of the ~10-op
+// v_div_scale/v_rcp/v_div_fmas/v_div_fixup sequence of a general division.
+__device__ __forceinline__ double div_const(double x, double d, double inv_d) {
+    double q = x * inv_d;
+    double r = fma(-q, d, x);
+    return fma(r, inv_d, q);
+}
+
 __device__ __forceinline__ void cars_obs(const double* xs, double* o) {
-#pragma clang fp contract(off)
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-        o[2 * i] = xs[2 * i] / 100.0;
-        o[2 * i + 1] = xs[2 * i + 1] / 30.0;
+        o[2 * i] = div_const(xs[2 * i], 100.0, 1.0 / 100.0);       // obs[::2] /= 100 (:156)
+        o[2 * i + 1] = div_const(xs[2 * i + 1], 30.0, 1.0 / 30.0);  // obs[1::2] /= 30 (:157)
     }
 }
 

@@ -22,7 +22,7 @@ __device__ __forceinline__ void load_state(const double* x, int64_t B, int64_t i
 template <int MODE>
 __device__ __forceinline__ void store_state(double* x, int64_t B, int64_t i, const double* xs) {
 #pragma unroll
-    for (int k = 0; k < Dims<MODE, 1>::NS; ++k) x[k * B + i] = xs[k];
+    for (int k = 0; k < Dims<MODE, 1>::NS; ++k) st_out(&x[k * B + i], xs[k]);
 }
 
 template <int MODE>
@@ -31,12 +31,12 @@ __device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double*
     double o[NO];
     env_obs<MODE>(xs, o);
     if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
-        float2* ov = reinterpret_cast<float2*>(obs + i * NO);  // 40 B rows, 8 B aligned
+        float* ov = obs + i * NO;  // 40 B rows, 8 B aligned
 #pragma unroll
-        for (int k = 0; k < NO / 2; ++k) ov[k] = make_float2((float)o[2 * k], (float)o[2 * k + 1]);
+        for (int k = 0; k < NO / 2; ++k) st_out2(ov + 2 * k, (float)o[2 * k], (float)o[2 * k + 1]);
     } else {
 #pragma unroll
-        for (int k = 0; k < NO; ++k) obs[i * NO + k] = (float)o[k];
+        for (int k = 0; k < NO; ++k) st_out(&obs[i * NO + k], (float)o[k]);
     }
 }
 
@@ -47,8 +47,8 @@ __global__ void __launch_bounds__(kBlock) k_env_reset(rcbf_params prm, int64_t B
                                                       int32_t* __restrict__ step, uint32_t* __restrict__ episode,
                                                       float* __restrict__ obs_out) {
     using D = Dims<MODE, 1>;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= B) return;
+    int64_t i = env_index();
+    if (i < 0 || i >= B) return;
     if (mask && !mask[i]) return;
     double xs[D::NS], a;
     int st;
@@ -70,8 +70,8 @@ __global__ void __launch_bounds__(kBlock) k_env_step(rcbf_params prm, int64_t B,
                                                      uint8_t* __restrict__ done, uint8_t* __restrict__ goal_met,
                                                      int auto_reset, uint64_t seed, int64_t off) {
     using D = Dims<MODE, 1>;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= B) return;
+    int64_t i = env_index();
+    if (i < 0 || i >= B) return;
     double xs[D::NS];
     load_state<MODE>(x, B, i, xs);
     double a = aux[i];
@@ -122,8 +122,15 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B
                                                       int32_t* __restrict__ status_out, int32_t* fail_flag,
                                                       int auto_reset, uint64_t seed, int64_t off) {
     using D = Dims<MODE, K>;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= B) return;
+    int64_t i = env_index();
+    if (i < 0 || i >= B) return;
+#if RCBF_STAMPS
+    unsigned long long* stamps = reinterpret_cast<unsigned long long*>(status_out);
+    status_out = nullptr;
+#else
+    unsigned long long* stamps = nullptr;
+#endif
+    RCBF_STAMP(stamps, 0, false);
     double xs[D::NS];
     load_state<MODE>(x, B, i, xs);
     double a = aux[i];
@@ -139,19 +146,22 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B
     float rew, cst;
     bool dn, gm;
     int status;
+    RCBF_STAMP(stamps, 1, true);
     safe_step_one<SOLVER, MODE, K>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
-                                   seed, off);
+                                   seed, off, stamps);
     store_state<MODE>(x, B, i, xs);
-    aux[i] = a;
-    step[i] = st;
+    st_out(&aux[i], a);
+    st_out(&step[i], st);
     store_obs32<MODE>(obs_out, i, xs);
 #pragma unroll
-    for (int c = 0; c < D::NU; ++c) u_out[i * D::NU + c] = uf[c];
-    reward[i] = rew;
-    cost[i] = cst;
-    done[i] = dn;
-    if (goal_met) goal_met[i] = gm;
+    for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
+    st_out(&reward[i], rew);
+    st_out(&cost[i], cst);
+    st_out(&done[i], (uint8_t)dn);
+    if (goal_met) st_out(&goal_met[i], (uint8_t)gm);
+    RCBF_STAMP(stamps, 6, false);
     report(status, status_out, i, fail_flag);
+    RCBF_STAMP(stamps, 7, true);
 }
 
 template <int MODE, int K>
@@ -163,8 +173,8 @@ __global__ void __launch_bounds__(kBlock) k_safe_rollout(rcbf_params prm, int64_
                                                          int32_t* __restrict__ n_done, int32_t* fail_flag,
                                                          uint64_t seed, int64_t off) {
     using D = Dims<MODE, K>;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= B) return;
+    int64_t i = env_index();
+    if (i < 0 || i >= B) return;
     double xs[D::NS];
     load_state<MODE>(x, B, i, xs);
     double a = aux[i];
@@ -218,10 +228,10 @@ int rcbf_env_reset(const rcbf_params* prm, int64_t B, const uint8_t* mask, const
     if (!x || !aux || !step) return RCBF_E_NULL;
     if (obs_out && (((uintptr_t)obs_out) & 7)) return RCBF_E_BAD_SHAPE;
     if (prm->mode == RCBF_MODE_SIMULATED_CARS)
-        hipLaunchKernelGGL((k_env_reset<RCBF_MODE_SIMULATED_CARS>), dim3(grid_for(B)), dim3(kBlock), 0, stream, *prm,
+        hipLaunchKernelGGL((k_env_reset<RCBF_MODE_SIMULATED_CARS>), dim3(grid_for_envs(B)), dim3(kBlock), 0, stream, *prm,
                            B, mask, noise, seed, env_offset, x, aux, step, episode, obs_out);
     else
-        hipLaunchKernelGGL((k_env_reset<RCBF_MODE_UNICYCLE>), dim3(grid_for(B)), dim3(kBlock), 0, stream, *prm, B,
+        hipLaunchKernelGGL((k_env_reset<RCBF_MODE_UNICYCLE>), dim3(grid_for_envs(B)), dim3(kBlock), 0, stream, *prm, B,
                            mask, noise, seed, env_offset, x, aux, step, episode, obs_out);
     return launch_status();
 }
@@ -235,7 +245,7 @@ int rcbf_env_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int
     if (B == 0) return 0;
     if (!x || !aux || !step || !action || !reward || !cost || !done) return RCBF_E_NULL;
     if (obs_out && (((uintptr_t)obs_out) & 7)) return RCBF_E_BAD_SHAPE;
-    dim3 g(grid_for(B)), b(kBlock);
+    dim3 g(grid_for_envs(B)), b(kBlock);
 #define RCBF_ENV_L(MODE, A)                                                                                       \
     hipLaunchKernelGGL((k_env_step<MODE, A>), g, b, 0, stream, *prm, B, x, aux, step, episode, (const A*)action, \
                        obs64_out, obs_out, reward, cost, done, goal_met, auto_reset, seed, env_offset)
@@ -263,7 +273,7 @@ int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, in
     if (B == 0) return 0;
     if (!x || !aux || !step || !u_rl || !obs_out || !u_out || !reward || !cost || !done) return RCBF_E_NULL;
     if (((uintptr_t)obs_out) & 7) return RCBF_E_BAD_SHAPE;  // float2 row stores
-    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0,
+    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0,
                                           stream, *prm, B, x, aux, step, episode, u_rl, mu, sigma, obs_out, u_out,
                                           reward, cost, done, goal_met, status_out, fail_flag, auto_reset, seed,
                                           env_offset));
@@ -278,7 +288,7 @@ int rcbf_safe_rollout(const rcbf_params* prm, int64_t B, int32_t K, double* x, d
     if (B == 0 || K == 0) return 0;
     if (!x || !aux || !step || !u_rl || !reward_sum || !cost_sum || !n_done) return RCBF_E_NULL;
     if (obs_out && (((uintptr_t)obs_out) & 7)) return RCBF_E_BAD_SHAPE;
-    RCBF_DISPATCH_MODE(prm, hipLaunchKernelGGL((k_safe_rollout<MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0,
+    RCBF_DISPATCH_MODE(prm, hipLaunchKernelGGL((k_safe_rollout<MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0,
                                                stream, *prm, B, K, x, aux, step, episode, u_rl, obs_out, reward_sum,
                                                cost_sum, n_done, fail_flag, seed, env_offset));
     return launch_status();

@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(kBlock) k_safe_action_bwd(rcbf_params prm, int
     float xs[D::NS], us[NU], m[D::NS], s[D::NS], uf[NU];
     load_layer_inputs<MODE, K>(i, x, u, mu, sigma, xs, us, m, s);
     LayerState<MODE, K> L;
-    layer_forward<SOLVER, MODE, K>(prm, xs, us, m, s, uf, L);
+    layer_forward<SOLVER, MODE, K, true>(prm, xs, us, m, s, uf, L);
     double pd[N];
     diff_P<MODE>(pd);
     // active rows (slots) of the solution

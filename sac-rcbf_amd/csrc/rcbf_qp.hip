@@ -77,7 +77,10 @@ __global__ void __launch_bounds__(kBlock) k_cascade(rcbf_params prm, int64_t B, 
     PMat<D::N, true> pm;
     pmat_set_diag<D::N>(pm, pd);
     QPResult<D::N, D::M> res;
-    qp_solve<SOLVER, D::N, D::M, true, double>(pm, q, G, h, prm.max_iter, prm.eps, res);
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && SOLVER == RCBF_SOLVER_ACTIVE_SET)
+        cars_qp_1d<double>(pm, G, h, res.z, res.status);
+    else
+        qp_solve<SOLVER, D::N, D::M, true, double>(pm, q, G, h, prm.max_iter, prm.eps, res);
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) u_out[i * D::NU + c] = res.z[c];
     report(res.status, status_out, i, fail_flag);
