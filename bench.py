@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extra", action="store_true", help="also time the K-step rollout kernel and big batches")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches (for PMC counter passes)")
     return ap.parse_args()
 
 
@@ -136,16 +137,22 @@ def main():
     # warmup (eager), then capture S fused steps into one hipGraph
     steps(max(args.warmup, 1))
     torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream(device=dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(s):
-        steps(2)  # warm the side stream before capture
-    torch.cuda.current_stream(dev).wait_stream(s)
-    with torch.cuda.graph(graph):
-        steps(S)
-    for _ in range(2):
-        graph.replay()
+    if args.no_graph:
+        class _Eager:
+            def replay(self):
+                steps(S)
+        graph = _Eager()
+    else:
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            steps(2)  # warm the side stream before capture
+        torch.cuda.current_stream(dev).wait_stream(s)
+        with torch.cuda.graph(graph):
+            steps(S)
+        for _ in range(2):
+            graph.replay()
     torch.cuda.synchronize()
     env.check_failures()
 

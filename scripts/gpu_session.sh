@@ -29,9 +29,13 @@ for step in "$@"; do
     prof)   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
               python3 bench.py --no-cpu-baseline ;;
     pmcf)   run pmcf 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-              python3 bench.py --no-cpu-baseline --steps 50 --warmup 5 ;;
+              python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 ;;
     pmcw)   run pmcw 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-              python3 bench.py --no-cpu-baseline --steps 50 --warmup 5 ;;
+              python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 ;;
+    pmcv)   run pmcv 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc_valu" -o run -- \
+              python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 ;;
+    profu)  run profu 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profu" -o run -- \
+              python3 bench.py --no-cpu-baseline --env Unicycle --hazards 3 ;;
     *) log "unknown step $step" ;;
   esac
 done
