@@ -96,6 +96,22 @@ def cpu_baseline(env_name, hazards, seconds):
                       f"{eN:.1f} s on {threads_all} threads; 1 thread: {v1:.4g} steps/s ({n1} steps)"}
 
 
+def pmc_traffic(env_name, B):
+    """HBM bytes per launch of k_safe_step from the committed rocprofv3 PMC
+    passes (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, gfx950
+    corrections) for this exact workload, newest round first; None if absent."""
+    import glob
+    short = "cars" if env_name == "SimulatedCars" else "unicycle3"
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{short}_B{B}.json")),
+                       reverse=True):
+        try:
+            rec = json.load(open(path))
+            return float(rec["traffic_bytes"]), os.path.relpath(path, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -184,6 +200,7 @@ def main():
     value = total_steps / el
     bps = BYTES_PER_STEP[args.env]
     achieved = B * bps / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.env, B)
     extra = {}
     if args.extra and rank == 0:
         extra = extra_measurements(env, layer, dev, args)
@@ -206,7 +223,8 @@ def main():
                    "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
                    "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": "k_safe_step", "bytes_per_launch": B * bps,
                      "kernel_ms": round(kern_ms, 5)},
     }
