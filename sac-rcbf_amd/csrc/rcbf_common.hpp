@@ -211,6 +211,8 @@ __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const floa
         L.qp.status = RCBF_QP_OK;
     } else if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && SOLVER == RCBF_SOLVER_ACTIVE_SET && !NEED_LAM) {
         cars_qp_1d<float>(pm, L.G, L.h, L.qp.z, L.qp.status);
+    } else if constexpr (MODE == RCBF_MODE_UNICYCLE && SOLVER == RCBF_SOLVER_ACTIVE_SET && !NEED_LAM) {
+        uni_qp_2d<K, float>(pm, L.G, L.h, L.qp.z, L.qp.status);
     } else {
         qp_solve<SOLVER, D::N, D::M, true, float>(pm, q, L.G, L.h, prm.max_iter, prm.eps, L.qp);
     }
@@ -278,12 +280,14 @@ __device__ __forceinline__ void state_from_env(const double* xs, float* s32) {
 
 // One fused safe step for one env (shared by k_safe_step and k_safe_rollout).
 // The episode counter is only touched when the env resets.
+// obs_cache (unicycle): cos/sin/goal distance of the post-step state, valid
+// unless the env was reset (then obs_cache[3] = 0 and the obs is recomputed).
 template <int SOLVER, int MODE, int K>
 __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i, double* xs, double& a, int& st,
                                               uint32_t* episode, const float* us, const float* m, const float* s,
                                               float* uf, float& rew, float& cst, bool& dn, bool& gm, int& status,
                                               int auto_reset, uint64_t seed, int64_t off,
-                                              unsigned long long* stamps = nullptr) {
+                                              unsigned long long* stamps = nullptr, double* obs_cache = nullptr) {
     using D = Dims<MODE, K>;
     float s32[D::NS];
     state_from_env<MODE>(xs, s32);
@@ -320,12 +324,19 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
         cst = (float)o.cost;
         dn = o.done;
         gm = o.goal;
+        if (obs_cache) {
+            obs_cache[0] = o.c;
+            obs_cache[1] = o.s;
+            obs_cache[2] = o.gd;
+            obs_cache[3] = 1.0;
+        }
     }
     RCBF_STAMP(stamps, 5, false);
     if (auto_reset && dn) {
         uint32_t ep = episode ? episode[i] + 1u : 0u;
         if (episode) episode[i] = ep;
         env_reset_one<MODE>(nullptr, i, seed, off, ep, xs, a, st);
+        if (obs_cache) obs_cache[3] = 0.0;
     }
 }
 

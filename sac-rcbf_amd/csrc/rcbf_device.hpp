@@ -23,8 +23,21 @@ namespace rcbf {
 
 constexpr double kInf = __builtin_huge_val();
 
+// fp64 reciprocal: v_rcp_f64 + two Newton steps (error ~1 ulp), no
+// div_scale/div_fixup chain.  rcp64(0) = inf.
+__device__ __forceinline__ double rcp64(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    return (d == 0.0) ? __builtin_copysign(__builtin_huge_val(), d) : r;
+}
+
 // ---------------------------------------------------------------------------
 // small fixed-size linear algebra (compile-time sizes -> registers)
+// (solver intermediates use rcp64: they are our own algorithm's quantities,
+// and the final results are exact KKT solutions either way)
 // ---------------------------------------------------------------------------
 template <int N>
 __device__ __forceinline__ double dotd(const double* a, const double* b) {
@@ -40,7 +53,7 @@ __device__ __forceinline__ double dotd(const double* a, const double* b) {
 template <int N>
 __device__ __forceinline__ bool ldl_solve(double S[N][N], const double* w, double* r) {
     double L[N][N];
-    double D[N];
+    double D[N], Dinv[N];
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -49,7 +62,8 @@ __device__ __forceinline__ bool ldl_solve(double S[N][N], const double* w, doubl
         for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k] * D[k];
         ok = ok && (d > 0.0);
         D[j] = d;
-        double inv = 1.0 / d;
+        double inv = rcp64(d);
+        Dinv[j] = inv;
 #pragma unroll
         for (int i = j + 1; i < N; ++i) {
             double v = S[i][j];
@@ -68,7 +82,7 @@ __device__ __forceinline__ bool ldl_solve(double S[N][N], const double* w, doubl
     }
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {
-        double v = y[i] / D[i];
+        double v = y[i] * Dinv[i];
 #pragma unroll
         for (int k = i + 1; k < N; ++k) v -= L[k][i] * r[k];
         r[i] = v;
@@ -80,6 +94,7 @@ __device__ __forceinline__ bool ldl_solve(double S[N][N], const double* w, doubl
 // Gaussian elimination with partial pivoting, fully unrolled.
 template <int N>
 __device__ __forceinline__ void gauss_solve(double A[N][N], double* b, double* x) {
+    double pinv[N];
 #pragma unroll
     for (int c = 0; c < N; ++c) {
         // pivot: swap the largest |A[r][c]|, r >= c, into row c (select-based)
@@ -96,7 +111,8 @@ __device__ __forceinline__ void gauss_solve(double A[N][N], double* b, double* x
             b[c] = sw ? bb : a;
             b[r] = sw ? a : bb;
         }
-        double inv = 1.0 / A[c][c];
+        double inv = rcp64(A[c][c]);
+        pinv[c] = inv;
 #pragma unroll
         for (int r = c + 1; r < N; ++r) {
             double f = A[r][c] * inv;
@@ -110,19 +126,8 @@ __device__ __forceinline__ void gauss_solve(double A[N][N], double* b, double* x
         double v = b[i];
 #pragma unroll
         for (int k = i + 1; k < N; ++k) v -= A[i][k] * x[k];
-        x[i] = v / A[i][i];
+        x[i] = v * pinv[i];
     }
-}
-
-// fp64 reciprocal: v_rcp_f64 + two Newton steps (error ~1 ulp), no
-// div_scale/div_fixup chain.  rcp64(0) = inf.
-__device__ __forceinline__ double rcp64(double d) {
-    double r = __builtin_amdgcn_rcp(d);
-    double e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    return (d == 0.0) ? __builtin_copysign(__builtin_huge_val(), d) : r;
 }
 
 // fp32 a / b, correctly rounded, via one fp64 reciprocal of b: the fp64
@@ -402,13 +407,13 @@ __device__ __forceinline__ void gi_solve(const PMat<N, DIAG>& pm, const double* 
             double gz = dotd<N>(gp, zdir);
             double gPg = dotd<N>(gp, Pg);
             double t2 = kInf;
-            if (A.n < N && gz < -1e-13 * gPg) t2 = (dotd<N>(gp, x) - hp) / (-gz);
+            if (A.n < N && gz < -1e-13 * gPg) t2 = (dotd<N>(gp, x) - hp) * rcp64(-gz);
             double t1 = kInf;
             int kdrop = -1;
 #pragma unroll
             for (int s = 0; s < N; ++s) {
                 bool cand = (s < A.n) && (r[s] > 1e-14);
-                double tt = cand ? A.lam[s] / r[s] : kInf;
+                double tt = cand ? A.lam[s] * rcp64(r[s]) : kInf;
                 bool better = cand && (tt < t1);
                 t1 = better ? tt : t1;
                 kdrop = better ? s : kdrop;
@@ -820,7 +825,7 @@ __device__ __forceinline__ void enum2_solve(const PMat<2, true>& pm, const R (*G
         // z = P^-1 g h / (g P^-1 g')
         double nrm = fma(g0[r] * pi0, g0[r], g1[r] * pi1 * g1[r]);
         bool ok = nrm > 1e-300;
-        double f = ok ? hh[r] / nrm : 0.0;
+        double f = ok ? hh[r] * rcp64(nrm) : 0.0;
         consider(pi0 * g0[r] * f, pi1 * g1[r] * f, 1u << r, ok);
     }
 #pragma unroll
@@ -829,7 +834,7 @@ __device__ __forceinline__ void enum2_solve(const PMat<2, true>& pm, const R (*G
         for (int s = r + 1; s < M; ++s) {
             double det = g0[r] * g1[s] - g1[r] * g0[s];
             bool ok = fabs(det) > 1e-12;
-            double inv = ok ? 1.0 / det : 0.0;
+            double inv = ok ? rcp64(det) : 0.0;
             double z0 = (hh[r] * g1[s] - hh[s] * g1[r]) * inv;
             double z1 = (g0[r] * hh[s] - g0[s] * hh[r]) * inv;
             consider(z0, z1, (1u << r) | (1u << s), ok);
@@ -857,11 +862,12 @@ __device__ __forceinline__ void enum2_solve(const PMat<2, true>& pm, const R (*G
     double la = 0.0, lb = 0.0;
     if (rb >= 0) {  // [ga gb] [la lb]' = -Pz  (2x2, Cramer)
         double det = ga0 * gb1 - gb0 * ga1;
-        la = (-Pz0 * gb1 + Pz1 * gb0) / det;
-        lb = (-ga0 * Pz1 + ga1 * Pz0) / det;
+        double idet = rcp64(det);
+        la = (-Pz0 * gb1 + Pz1 * gb0) * idet;
+        lb = (-ga0 * Pz1 + ga1 * Pz0) * idet;
     } else if (ra >= 0) {
         double nn = ga0 * ga0 + ga1 * ga1;
-        la = -(Pz0 * ga0 + Pz1 * ga1) / nn;
+        la = -(Pz0 * ga0 + Pz1 * ga1) * rcp64(nn);
     }
 #pragma unroll
     for (int r = 0; r < M; ++r) out.lam[r] = (r == ra) ? la : ((r == rb) ? lb : 0.0);
@@ -1032,6 +1038,146 @@ __device__ __forceinline__ void cars_qp_1d(const PMat<2, true>& pm, const R (*G)
                                                                                : RCBF_QP_NONFINITE);
 }
 
+// Exact solver for the UNICYCLE QP structure (both formulations), z = (u0, u1, eps):
+//   rows j < K:  g_j0 u0 + g_j1 u1 + g_j2 eps <= h_j  with g_j2 < 0 (slack column)
+//   rows K..K+3: u0 <= U0, -u0 <= .., u1 <= U1, -u1 <= ..  (the actuator box)
+//   objective    1/2 (p0 u0^2 + p1 u1^2 + p2 eps^2)
+// As for cars, eps*(u) = max(0, max_j e_j(u)) with affine e_j(u) = a_j.u + b_j,
+// leaving the 2-D convex piecewise quadratic
+//   phi(u) = p0 u0^2 + p1 u1^2 + p2 eps*(u)^2   over the box.
+// Stage 1, box-free optimum: it is u = 0, the stationary point of one piece
+// (Sherman-Morrison on diag(p0,p1) + p2 a a'), the minimiser on one kink line
+// e_i = e_j, or a triple point e_i = e_j = e_l (phi is differentiable where an
+// e_j crosses 0); the argmin of phi over these candidates is exact.
+// Stage 2: if that point u_f leaves the box, the constrained optimum lies on
+// a FACING edge -- one whose constraint u_f violates (otherwise a small step
+// from it toward u_f stays feasible and strictly lowers phi).  So one u0-edge
+// (u0 = clamp(u_f0)) and one u1-edge (u1 = clamp(u_f1)) suffice; each is a
+// 1-D problem solved exactly like cars_qp_1d (clamped stationary points and
+// kinks).  For a coordinate u_f does not violate, the "edge" is an interior
+// line whose candidates are still feasible points -- harmless -- so both
+// edges run branch-free in every lane.
+template <int K, typename R>
+__device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[3], const R* h, double* z,
+                                          int& status) {
+    const double p0 = pm.P[0][0], p1 = pm.P[1][1], p2 = pm.P[2][2];
+    const double ip0 = pm.Pinv[0][0], ip1 = pm.Pinv[1][1];
+    double a0[K], a1[K], b[K];
+    bool finite = true;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const double inv = rcp64((double)G[j][2]);
+        a0[j] = -(double)G[j][0] * inv;
+        a1[j] = -(double)G[j][1] * inv;
+        b[j] = (double)h[j] * inv;
+        finite = finite && isfinite(a0[j]) && isfinite(a1[j]) && isfinite(b[j]);
+    }
+    const double U0 = (double)h[K] * rcp64((double)G[K][0]);
+    const double L0 = (double)h[K + 1] * rcp64((double)G[K + 1][0]);
+    const double U1 = (double)h[K + 2] * rcp64((double)G[K + 2][1]);
+    const double L1 = (double)h[K + 3] * rcp64((double)G[K + 3][1]);
+    auto eps_of = [&](double u0, double u1) {
+        double e = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) e = fmax(e, fma(a0[j], u0, fma(a1[j], u1, b[j])));
+        return e;
+    };
+    auto phi = [&](double u0, double u1) {
+        double e = eps_of(u0, u1);
+        return fma(p0 * u0, u0, fma(p1 * u1, u1, p2 * e * e));
+    };
+    double bu0 = 0.0, bu1 = 0.0, bf = phi(0.0, 0.0);
+    auto take = [&](double u0, double u1) {
+        double f = phi(u0, u1);
+        bool t = f < bf;  // NaN candidates never win
+        bu0 = t ? u0 : bu0;
+        bu1 = t ? u1 : bu1;
+        bf = t ? f : bf;
+    };
+    // stage 1: box-free candidates
+#pragma unroll
+    for (int j = 0; j < K; ++j) {  // piece j: (diag(p0,p1) + p2 a a') u = -p2 b a
+        double w0 = a0[j] * ip0, w1 = a1[j] * ip1;
+        double sden = fma(p2, fma(a0[j], w0, a1[j] * w1), 1.0);
+        double f = -p2 * b[j] * rcp64(sden);
+        take(f * w0, f * w1);
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+#pragma unroll
+        for (int j = i + 1; j < K; ++j) {  // kink line (a_i - a_j).u = b_j - b_i, minimise along it
+            double d0 = a0[i] - a0[j], d1 = a1[i] - a1[j], c = b[j] - b[i];
+            double dd = fma(d0, d0, d1 * d1);
+            if (dd > 1e-300) {
+                double idd = rcp64(dd);
+                double q0 = c * d0 * idd, q1 = c * d1 * idd;  // a point on the line
+                double n0 = -d1, n1 = d0;                     // its direction
+                double ea = fma(a0[i], q0, fma(a1[i], q1, b[i])), an = fma(a0[i], n0, a1[i] * n1);
+                double num = fma(p0 * q0, n0, fma(p1 * q1, n1, p2 * ea * an));
+                double den = fma(p0 * n0, n0, fma(p1 * n1, n1, p2 * an * an));
+                double t = -num * rcp64(den);
+                take(fma(t, n0, q0), fma(t, n1, q1));
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+#pragma unroll
+        for (int j = i + 1; j < K; ++j) {
+#pragma unroll
+            for (int l = j + 1; l < K; ++l) {  // triple point e_i = e_j = e_l
+                double m00 = a0[i] - a0[j], m01 = a1[i] - a1[j], r0 = b[j] - b[i];
+                double m10 = a0[i] - a0[l], m11 = a1[i] - a1[l], r1 = b[l] - b[i];
+                double det = fma(m00, m11, -m01 * m10);
+                if (fabs(det) > 1e-300) {
+                    double id = rcp64(det);
+                    take((r0 * m11 - r1 * m01) * id, (m00 * r1 - m10 * r0) * id);
+                }
+            }
+        }
+    }
+    const bool inbox = (bu0 >= L0) && (bu0 <= U0) && (bu1 >= L1) && (bu1 <= U1);
+    {
+        // stage 2 (branch-free): the facing u0-edge and u1-edge
+        const double v0 = fmin(fmax(bu0, L0), U0), v1 = fmin(fmax(bu1, L1), U1);
+        bf = inbox ? bf : __builtin_huge_val();  // an out-of-box stage-1 point must not win
+        auto edge = [&](bool fix0, double v, double lo, double hi) {
+            // free coordinate y in [lo, hi]; e_j = al_j y + be_j
+            double al[K], be[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                al[j] = fix0 ? a1[j] : a0[j];
+                be[j] = fix0 ? fma(a0[j], v, b[j]) : fma(a1[j], v, b[j]);
+            }
+            const double pf = fix0 ? p1 : p0;
+            auto cand = [&](double y) {
+                y = fmin(fmax(y, lo), hi);
+                if (fix0)
+                    take(v, y);
+                else
+                    take(y, v);
+            };
+            cand(0.0);
+#pragma unroll
+            for (int j = 0; j < K; ++j) cand(-(p2 * al[j] * be[j]) * rcp64(fma(p2 * al[j], al[j], pf)));
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int j = i + 1; j < K; ++j) {
+                    double den = al[i] - al[j];
+                    if (den != 0.0) cand((be[j] - be[i]) * rcp64(den));
+                }
+        };
+        edge(true, v0, L1, U1);
+        edge(false, v1, L0, U0);
+    }
+    z[0] = bu0;
+    z[1] = bu1;
+    z[2] = eps_of(bu0, bu1);
+    const bool ok = isfinite(z[0]) && isfinite(z[1]) && isfinite(z[2]) && bf < __builtin_huge_val();
+    status = !finite ? RCBF_QP_NONFINITE : (ok && L0 <= U0 && L1 <= U1 ? RCBF_QP_OK : RCBF_QP_INFEASIBLE);
+}
+
 // Compile-time solver choice (the host dispatches on rcbf_params.solver):
 //   RCBF_SOLVER_ACTIVE_SET: exact -- KKT enumeration for n = 2, Goldfarb-Idnani
 //                           for n = 3 or a full P;
@@ -1178,8 +1324,10 @@ __device__ __forceinline__ void uni_rows_diff(const rcbf_params& prm, const floa
 #pragma clang fp contract(off)
     const float lp = (float)prm.l_p, g = (float)prm.gamma_b;
     // fp32 cos/sin, correctly rounded from fp64 (torch's SLEEF is within 1 ulp)
-    float c = (float)cos((double)xs[2]);
-    float s = (float)sin((double)xs[2]);
+    double sd, cd;
+    sincos((double)xs[2], &sd, &cd);  // one shared range reduction
+    float c = (float)cd;
+    float s = (float)sd;
     float px = xs[0] + lp * c, py = xs[1] + lp * s;
     float g00 = c, g01 = -s * lp, g10 = s, g11 = c * lp;
     float mupx = g01 * mu[2] + mu[0], mupy = g11 * mu[2] + mu[1];
@@ -1221,7 +1369,8 @@ __device__ __forceinline__ void uni_rows_cascade(const rcbf_params& prm, const d
                                                  double* h) {
 #pragma clang fp contract(off)
     const double lp = prm.l_p, g = prm.gamma_b, kd = prm.k_d;
-    double c = cos(xs[2]), s = sin(xs[2]);
+    double c, s;
+    sincos(xs[2], &s, &c);
     double px = xs[0] + lp * c, py = xs[1] + lp * s;
     double g00 = c, g01 = -s * lp, g10 = s, g11 = c * lp;
     double mpx = mu[0] + lp * (-s) * mu[2], mpy = mu[1] + lp * c * mu[2];
@@ -1327,11 +1476,29 @@ __device__ __forceinline__ double uni_goal_dist(const double* xs) {
 }
 
 // UnicycleEnv.get_obs (unicycle_env.py:215-231) + obs_compass (:260-277)
+// obs from precomputed cos/sin of theta and goal distance (the env step
+// already has them for the new state)
+__device__ __forceinline__ void uni_obs_cs(const double* xs, double c, double s, double gd, double* o) {
+#pragma clang fp contract(off)
+    double r0 = 2.5 - xs[0], r1 = 2.5 - xs[1];
+    double v0 = r0 * c + r1 * s;
+    double v1 = r0 * (-s) + r1 * c;
+    double nrm = sqrt(v0 * v0 + v1 * v1) + 0.001;
+    o[0] = xs[0];
+    o[1] = xs[1];
+    o[2] = c;
+    o[3] = s;
+    o[4] = v0 / nrm;
+    o[5] = v1 / nrm;
+    o[6] = exp(-gd);
+}
+
 __device__ __forceinline__ void uni_obs(const double* xs, double* o) {
 #pragma clang fp contract(off)
     double r0 = 2.5 - xs[0], r1 = 2.5 - xs[1];
     double gd = sqrt(r0 * r0 + r1 * r1);
-    double c = cos(xs[2]), s = sin(xs[2]);
+    double c, s;
+    sincos(xs[2], &s, &c);
     double v0 = r0 * c + r1 * s;
     double v1 = r0 * (-s) + r1 * c;
     double nrm = sqrt(v0 * v0 + v1 * v1) + 0.001;
@@ -1349,6 +1516,7 @@ struct UniStepOut {
     double cost;
     bool done;
     bool goal;
+    double c, s, gd;  // cos/sin of the new theta and the new goal distance (for the obs)
 };
 
 // UnicycleEnv.step/_step (unicycle_env.py:46-111): clip to +-1 after the
@@ -1362,16 +1530,21 @@ __device__ __forceinline__ void uni_env_step(const rcbf_params& prm, double* xs,
     A a1c = action[1] < (A)(-1) ? (A)(-1) : (action[1] > (A)1 ? (A)1 : action[1]);
     double a0 = (double)a0c, a1 = (double)a1c;
     const double dt = 0.02;
-    double c = cos(xs[2]), s = sin(xs[2]);
+    double c, s;
+    sincos(xs[2], &s, &c);
     xs[0] += dt * (0.0 + c * a0);
     xs[1] += dt * (0.0 + s * a0);
     xs[2] += dt * (0.0 + a1);
-    double c2 = cos(xs[2]), s2 = sin(xs[2]);
+    double c2, s2;
+    sincos(xs[2], &s2, &c2);
     const double k = dt * 0.1;
     xs[0] -= (k * c2) * c2;
     xs[1] -= (k * s2) * c2;
+    o.c = c2;
+    o.s = s2;
     step += 1;
     double d = uni_goal_dist(xs);
+    o.gd = d;
     double reward = last_dist - d;
     last_dist = d;
     bool goal = d <= 0.3;

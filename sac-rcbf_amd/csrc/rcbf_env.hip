@@ -26,10 +26,18 @@ __device__ __forceinline__ void store_state(double* x, int64_t B, int64_t i, con
 }
 
 template <int MODE>
-__device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double* xs) {
+__device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double* xs,
+                                            const double* obs_cache = nullptr) {
     constexpr int NO = Dims<MODE, 1>::NO;
     double o[NO];
-    env_obs<MODE>(xs, o);
+    if constexpr (MODE == RCBF_MODE_UNICYCLE && (kAblate & 8) == 0) {
+        if (obs_cache && obs_cache[3] != 0.0)
+            uni_obs_cs(xs, obs_cache[0], obs_cache[1], obs_cache[2], o);
+        else
+            env_obs<MODE>(xs, o);
+    } else {
+        env_obs<MODE>(xs, o);
+    }
     if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
         float* ov = obs + i * NO;  // 40 B rows, 8 B aligned
 #pragma unroll
@@ -147,12 +155,13 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B
     bool dn, gm;
     int status;
     RCBF_STAMP(stamps, 1, true);
+    double oc[4] = {0.0, 0.0, 0.0, 0.0};
     safe_step_one<SOLVER, MODE, K>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
-                                   seed, off, stamps);
+                                   seed, off, stamps, oc);
     store_state<MODE>(x, B, i, xs);
     st_out(&aux[i], a);
     st_out(&step[i], st);
-    store_obs32<MODE>(obs_out, i, xs);
+    store_obs32<MODE>(obs_out, i, xs, oc);
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
     st_out(&reward[i], rew);

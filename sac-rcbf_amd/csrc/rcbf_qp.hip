@@ -79,6 +79,8 @@ __global__ void __launch_bounds__(kBlock) k_cascade(rcbf_params prm, int64_t B, 
     QPResult<D::N, D::M> res;
     if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && SOLVER == RCBF_SOLVER_ACTIVE_SET)
         cars_qp_1d<double>(pm, G, h, res.z, res.status);
+    else if constexpr (MODE == RCBF_MODE_UNICYCLE && SOLVER == RCBF_SOLVER_ACTIVE_SET)
+        uni_qp_2d<K, double>(pm, G, h, res.z, res.status);
     else
         qp_solve<SOLVER, D::N, D::M, true, double>(pm, q, G, h, prm.max_iter, prm.eps, res);
 #pragma unroll

@@ -12,7 +12,7 @@ import torch  # noqa: E402
 
 from rcbf_amd import _lib  # noqa: E402
 from rcbf_amd.diff_cbf_qp import CBFQPLayer  # noqa: E402
-from rcbf_amd.envs import BatchedSimulatedCarsEnv  # noqa: E402
+from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv  # noqa: E402
 
 
 class A:
@@ -20,12 +20,19 @@ class A:
 
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-env = BatchedSimulatedCarsEnv(B, seed=3)
+uni = len(sys.argv) > 2 and sys.argv[2] == "unicycle"
+if uni:
+    hz = np.array([[0., 0.], [-1., 1.], [-1., -1.]]) * 1.5
+    env = BatchedUnicycleEnv(B, seed=3, hazards_locations=hz)
+    rng = np.random.default_rng(0)
+    env.load_state(np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1))
+else:
+    env = BatchedSimulatedCarsEnv(B, seed=3)
 layer = CBFQPLayer(env, A(), gamma_b=20.0)
 o = env.make_outputs()
 nw = (B + 63) // 64
 st = torch.zeros(nw * 16, dtype=torch.int64, device="cuda")
-u = (torch.rand(B, 1, device="cuda") * 2 - 1).contiguous()
+u = (torch.rand(B, env.n_u, device="cuda") * 2 - 1).contiguous()
 lib = _lib.load()
 names = ["load", "get_state", "rows+norm", "QP", "env step", "obs+stores issued", "stores drained"]
 res = []
@@ -35,7 +42,7 @@ for rep in range(30):
     rc = lib.rcbf_safe_step(ctypes.byref(layer._prm), B, _lib.ptr(env.x), _lib.ptr(env.aux), _lib.ptr(env.step_count),
                             _lib.ptr(env.episode), _lib.ptr(u), None, None, _lib.ptr(env.obs), _lib.ptr(o["u"]),
                             _lib.ptr(o["reward"]), _lib.ptr(o["cost"]), _lib.ptr(o["done"]), None, _lib.ptr(st),
-                            None, 1, 1, 0, _lib.stream_of(torch.device("cuda")))
+                            None, 0 if uni else 1, 1, 0, _lib.stream_of(torch.device("cuda")))
     assert rc == 0
     torch.cuda.synchronize()
     if rep >= 10:
