@@ -1,0 +1,143 @@
+"""numpy restatements of the two closed-form QP solvers the HIP kernels use
+(sac-rcbf_amd/csrc/rcbf_device.hpp: cars_qp_1d, uni_qp_2d), vectorised over
+the batch.  Test infrastructure only: they let the CPU suite check the solver
+*algorithm* against oracle.qp_exact (the KKT enumeration that stands in for
+qpth / quadprog, diff_cbf_qp.py:136, cbf_qp.py:231) on many random states
+without a GPU.  The GPU kernels themselves are checked in test_gpu_parity.py.
+
+Both exploit the structure of the CBF-QP: the slack variable eps (weight
+P[-1,-1]) only appears in the CBF rows  G_j[:n_u] u - eps <= h_j  (G_j[-1]<0
+after normalisation), so for fixed u the optimal eps is
+max(0, max_j (a_j.u + b_j)), and the QP reduces to minimising the convex
+piecewise quadratic  phi(u) = sum p_k u_k^2 + p_eps max(0, a_j.u + b_j)^2
+over the box  u_min - u_rl <= u <= u_max - u_rl.
+"""
+import itertools
+
+import numpy as np
+
+
+def cars_qp_1d(Gn, hn, pd):
+    """SimulatedCars diff QP: variables (u, eps), rows [cbf0, cbf1, u<=U, -u<=-L].
+    The minimiser of the 1-D convex phi over [L, U] is the clamp of one of
+    {0, stationary point of each piece, kink}; take the best.  Rows are
+    (B,4,2) f32 after normalize_rows, pd = diag(P) in f64."""
+    G = Gn.astype(np.float64)
+    h = hn.astype(np.float64)
+    p0, p1 = pd
+    U = h[:, 2] / G[:, 2, 0]
+    L = h[:, 3] / G[:, 3, 0]
+    i0 = 1 / G[:, 0, 1]
+    i1 = 1 / G[:, 1, 1]
+    a0, b0 = -G[:, 0, 0] * i0, h[:, 0] * i0
+    a1, b1 = -G[:, 1, 0] * i1, h[:, 1] * i1
+    c1 = -(p1 * a0 * b0) / (p1 * a0 * a0 + p0)
+    c2 = -(p1 * a1 * b1) / (p1 * a1 * a1 + p0)
+    den = a0 - a1
+    c3 = np.where(den != 0, (b1 - b0) / np.where(den != 0, den, 1), 0)
+
+    def cl(u):
+        return np.minimum(np.maximum(u, L), U)
+
+    def eps(u):
+        return np.maximum(0, np.maximum(a0 * u + b0, a1 * u + b1))
+
+    def phi(u):
+        return p0 * u * u + p1 * eps(u) ** 2
+
+    C = np.stack([cl(np.zeros_like(U)), cl(c1), cl(c2), cl(c3)], 1)
+    f = np.stack([phi(C[:, k]) for k in range(4)], 1)
+    u = C[np.arange(len(U)), f.argmin(1)]
+    return np.stack([u, eps(u)], 1)
+
+
+def uni_qp_2d(Gn, hn, pd, K):
+    """Unicycle QP: variables (u0, u1, eps), rows [K cbf rows, 4 box rows].
+    Stage 1: box-free minimisers (origin, per-piece Sherman-Morrison
+    stationary points, minimisers on each kink line, triple points); the best
+    one is the unconstrained optimum of phi.  If it lies outside the box, the
+    constrained optimum lies on a facing edge (u0 or u1 fixed to its clamped
+    value); each edge is a 1-D problem solved like cars_qp_1d.
+    Returns ((B,3) z, in-box mask)."""
+    G = Gn.astype(np.float64)
+    h = hn.astype(np.float64)
+    p0, p1, p2 = pd
+    B = G.shape[0]
+    inv = 1 / G[:, :K, 2]
+    a0 = -G[:, :K, 0] * inv
+    a1 = -G[:, :K, 1] * inv
+    b = h[:, :K] * inv
+    U0 = h[:, K] / G[:, K, 0]
+    L0 = h[:, K + 1] / G[:, K + 1, 0]
+    U1 = h[:, K + 2] / G[:, K + 2, 1]
+    L1 = h[:, K + 3] / G[:, K + 3, 1]
+
+    def eps(u0, u1):
+        return np.maximum(0, (a0 * u0[:, None] + a1 * u1[:, None] + b).max(1))
+
+    def phi(u0, u1):
+        e = eps(u0, u1)
+        return p0 * u0 * u0 + p1 * u1 * u1 + p2 * e * e
+
+    C = [(np.zeros(B), np.zeros(B))]
+    for j in range(K):
+        w0 = a0[:, j] / p0
+        w1 = a1[:, j] / p1
+        s = 1 + p2 * (a0[:, j] * w0 + a1[:, j] * w1)
+        f = -p2 * b[:, j] / s
+        C.append((f * w0, f * w1))
+    for i in range(K):
+        for j in range(i + 1, K):
+            d0 = a0[:, i] - a0[:, j]
+            d1 = a1[:, i] - a1[:, j]
+            c = b[:, j] - b[:, i]
+            dd = d0 * d0 + d1 * d1
+            ok = dd > 1e-300
+            dd = np.where(ok, dd, 1)
+            q0, q1 = c * d0 / dd, c * d1 / dd
+            n0, n1 = -d1, d0
+            ea = a0[:, i] * q0 + a1[:, i] * q1 + b[:, i]
+            an = a0[:, i] * n0 + a1[:, i] * n1
+            num = p0 * q0 * n0 + p1 * q1 * n1 + p2 * ea * an
+            den = p0 * n0 * n0 + p1 * n1 * n1 + p2 * an * an
+            t = -num / np.where(den != 0, den, 1)
+            C.append((np.where(ok, q0 + t * n0, 0), np.where(ok, q1 + t * n1, 0)))
+    for i, j, l in itertools.combinations(range(K), 3):
+        m00 = a0[:, i] - a0[:, j]
+        m01 = a1[:, i] - a1[:, j]
+        r0 = b[:, j] - b[:, i]
+        m10 = a0[:, i] - a0[:, l]
+        m11 = a1[:, i] - a1[:, l]
+        r1 = b[:, l] - b[:, i]
+        det = m00 * m11 - m01 * m10
+        ok = np.abs(det) > 1e-300
+        det = np.where(ok, det, 1)
+        C.append((np.where(ok, (r0 * m11 - r1 * m01) / det, 0), np.where(ok, (m00 * r1 - m10 * r0) / det, 0)))
+    Fv = np.stack([phi(u0, u1) for u0, u1 in C], 1)
+    k = np.nanargmin(Fv, 1)
+    U0s = np.stack([c[0] for c in C], 1)[np.arange(B), k]
+    U1s = np.stack([c[1] for c in C], 1)[np.arange(B), k]
+    inb = (U0s >= L0) & (U0s <= U0) & (U1s >= L1) & (U1s <= U1)
+    best = np.full(B, np.inf)
+    bu0, bu1 = U0s.copy(), U1s.copy()
+    v0 = np.minimum(np.maximum(U0s, L0), U0)
+    v1 = np.minimum(np.maximum(U1s, L1), U1)
+    for fix0, v, lo, hi in [(True, v0, L1, U1), (False, v1, L0, U0)]:
+        al = a1 if fix0 else a0
+        be = (a0 * v[:, None] + b) if fix0 else (a1 * v[:, None] + b)
+        pf = p1 if fix0 else p0
+        ys = [np.zeros(B)] + [-(p2 * al[:, j] * be[:, j]) / (p2 * al[:, j] ** 2 + pf) for j in range(K)]
+        for i in range(K):
+            for j in range(i + 1, K):
+                den = al[:, i] - al[:, j]
+                ys.append(np.where(den != 0, (be[:, j] - be[:, i]) / np.where(den != 0, den, 1), 0))
+        for y in ys:
+            y = np.minimum(np.maximum(y, lo), hi)
+            u0 = v if fix0 else y
+            u1 = y if fix0 else v
+            f = phi(u0, u1)
+            t = (f < best) & ~inb
+            best = np.where(t, f, best)
+            bu0 = np.where(t, u0, bu0)
+            bu1 = np.where(t, u1, bu1)
+    return np.stack([bu0, bu1, eps(bu0, bu1)], 1), inb
