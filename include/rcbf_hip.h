@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 3
+#define RCBF_ABI_VERSION 4
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -135,12 +135,16 @@ int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom,
 /* ---------------------------------------------------------------------- */
 /* Environments (batched, device-resident, fp64 state like the numpy envs) */
 /* ---------------------------------------------------------------------- */
-/* Per-env state, COMPONENT-MAJOR (SoA):  x (n_s, B) f64, x[k*B + i] =
- * env_i.state[k];  aux (B,) f64 = env.t (cars) or env.last_goal_dist
+/* Per-env state, COMPONENT-PAIR-MAJOR:  x (n_s * B) f64, 16-byte aligned;
+ * components (2p, 2p+1) of env i at x[2*(p*B + i)] and x[2*(p*B + i) + 1]
+ * (one (B, 2) block per pair, so a lane moves 16 B per pair and a wavefront
+ * 1 KiB contiguous), and for odd n_s the last component at x[(n_s-1)*B + i].
+ * x = env_i.state;  aux (B,) f64 = env.t (cars) or env.last_goal_dist
  * (unicycle);  step (B,) i32 = env.episode_step;  episode (B,) u32 = reset
  * counter keying the per-env counter-based RNG (read/written only on reset).
  * Observations are row-major (B, n_o), the policy's input layout, 8-byte
- * aligned.  (For B = 1 the SoA and row-major layouts coincide.)  */
+ * aligned.  (For B = 1 the state layout is the state row itself.)
+ * A misaligned x or obs returns RCBF_E_BAD_SHAPE.  */
 
 /* SimulatedCarsEnv.reset (simulated_cars_env.py:108-125) / UnicycleEnv.reset
  * (unicycle_env.py:125-143) for the envs selected by mask [nullable: all].

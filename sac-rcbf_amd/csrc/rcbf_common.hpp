@@ -48,11 +48,23 @@ __device__ __forceinline__ int64_t env_index() {
 // Output store flavour of the env kernels (performance study knob):
 //   0 = plain stores (lines stay dirty in the XCD's L2 until the kernel-end
 //       write-back), 1 = write-through `sc1` stores (agent-scope relaxed
-//       atomic stores: the line leaves L2 as it is written), 2 = `nt` stores.
+//       atomic stores: the line leaves L2 as it is written), 2 = `nt` stores
+//       (default: with whole-line stores it is the fastest, profiles/r01).
 #ifndef RCBF_STORE_MODE
-#define RCBF_STORE_MODE 0
+#define RCBF_STORE_MODE 2
 #endif
 constexpr int kStoreMode = RCBF_STORE_MODE;
+// with RCBF_STORE_MODE=2: also store the staged observation chunks `nt`
+#ifndef RCBF_OBS_NT
+#define RCBF_OBS_NT 1
+#endif
+constexpr bool kObsNt = RCBF_OBS_NT;
+
+// 1 = store the safe action right after the QP so its write overlaps the env
+// step (otherwise all outputs are stored after the observation).
+#ifndef RCBF_EARLY_STORE
+#define RCBF_EARLY_STORE 0
+#endif
 
 template <typename T>
 __device__ __forceinline__ void st_out(T* p, T v) {
@@ -63,6 +75,52 @@ __device__ __forceinline__ void st_out(T* p, T v) {
     } else {
         *p = v;
     }
+}
+
+// 16-byte store (staged obs chunks), same flavours except sc1 -> plain
+__device__ __forceinline__ void st_out4(float* p, float4 v) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    if constexpr (kStoreMode == 2 && kObsNt) {
+        f4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<f4*>(p));
+    } else {
+        *reinterpret_cast<float4*>(p) = v;
+    }
+}
+
+// 16-byte f64 pair store (env state pairs)
+__device__ __forceinline__ void st_out2d(double* p, double a, double b) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    if constexpr (kStoreMode == 1) {
+        st_out(p, a);
+        st_out(p + 1, b);
+    } else if constexpr (kStoreMode == 2) {
+        d2 w = {a, b};
+        __builtin_nontemporal_store(w, reinterpret_cast<d2*>(p));
+    } else {
+        *reinterpret_cast<double2*>(p) = make_double2(a, b);
+    }
+}
+
+// Input load flavour: 0 = plain, 2 = `nt` (once-read streams)
+#ifndef RCBF_LOAD_MODE
+#define RCBF_LOAD_MODE 2
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_in(const T* p) {
+    if constexpr (RCBF_LOAD_MODE == 2)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+__device__ __forceinline__ double2 ld_in2(const double* p) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    d2 v;
+    if constexpr (RCBF_LOAD_MODE == 2)
+        v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(p));
+    else
+        v = *reinterpret_cast<const d2*>(p);
+    return make_double2(v.x, v.y);
 }
 
 // 8-byte pair store (obs rows): one dwordx2 store in every flavour
@@ -233,9 +291,12 @@ __device__ __forceinline__ void report(int status, int32_t* status_out, int64_t 
 // ---------------------------------------------------------------------------
 // environments
 // ---------------------------------------------------------------------------
-// Env state in HBM is component-major (SoA): x[k * B + i] is component k of
-// env i, so every component load/store of a wavefront is one contiguous
-// 512-byte access.  aux/step/episode are (B,) vectors.
+// Env state in HBM is component-PAIR-major: components (2p, 2p+1) of env i
+// sit at x[2 (p B + i)] and x[2 (p B + i) + 1] (a (B, 2) block per pair), and
+// an odd last component n_s-1 at x[(n_s-1) B + i].  Every lane moves 16 B per
+// pair, so a wavefront's pair load/store is one contiguous 1 KiB dwordx4
+// access (half the memory instructions of plain SoA).  For B = 1 the layout
+// is the state row itself.  aux/step/episode are (B,) vectors.
 template <int MODE>
 __device__ __forceinline__ void env_reset_one(const double* noise, int64_t i, uint64_t seed, int64_t off,
                                               uint32_t ep, double* xs, double& aux, int& st) {
@@ -287,7 +348,8 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
                                               uint32_t* episode, const float* us, const float* m, const float* s,
                                               float* uf, float& rew, float& cst, bool& dn, bool& gm, int& status,
                                               int auto_reset, uint64_t seed, int64_t off,
-                                              unsigned long long* stamps = nullptr, double* obs_cache = nullptr) {
+                                              unsigned long long* stamps = nullptr, double* obs_cache = nullptr,
+                                              float* u_out = nullptr) {
     using D = Dims<MODE, K>;
     float s32[D::NS];
     state_from_env<MODE>(xs, s32);
@@ -295,6 +357,11 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
     LayerState<MODE, K> L;
     layer_forward<SOLVER, MODE, K>(prm, s32, us, m, s, uf, L, stamps);
     status = L.qp.status;
+    // issue the safe-action store now so its write overlaps the env step
+    if (u_out) {
+#pragma unroll
+        for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
+    }
 #if RCBF_STAMPS
     {
         unsigned long long fb = __ballot(L.qp.iters == 1);

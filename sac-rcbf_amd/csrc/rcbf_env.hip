@@ -2,9 +2,9 @@
 // rcbf_env_reset, rcbf_env_step, rcbf_safe_step (the hot path bench.py
 // measures), rcbf_safe_rollout, version/ABI queries.
 //
-// Env state is component-major (SoA) in HBM: x[k * B + i].  One env per
-// lane; a wavefront's load or store of one component is a contiguous 512 B
-// (f64) or 256 B (f32) access.  The fused step reads x, t, step, u_RL and
+// Env state is component-PAIR-major in HBM (see rcbf_common.hpp): one env per
+// lane, each lane moves 16 B per component pair, and a wavefront's load or
+// store of one pair is one contiguous 1 KiB access (dwordx4).  The fused step reads x, t, step, u_RL and
 // writes x', t', step', obs (AoS, the policy's (B, n_o) input), u, reward,
 // cost, done; the episode counter is touched only on resets.
 #include "rcbf_common.hpp"
@@ -15,14 +15,22 @@ namespace {
 
 template <int MODE>
 __device__ __forceinline__ void load_state(const double* x, int64_t B, int64_t i, double* xs) {
+    constexpr int NS = Dims<MODE, 1>::NS;
 #pragma unroll
-    for (int k = 0; k < Dims<MODE, 1>::NS; ++k) xs[k] = x[k * B + i];
+    for (int p = 0; p < NS / 2; ++p) {
+        double2 v = ld_in2(&x[2 * (p * B + i)]);
+        xs[2 * p] = v.x;
+        xs[2 * p + 1] = v.y;
+    }
+    if constexpr (NS % 2) xs[NS - 1] = ld_in(&x[(NS - 1) * B + i]);
 }
 
 template <int MODE>
 __device__ __forceinline__ void store_state(double* x, int64_t B, int64_t i, const double* xs) {
+    constexpr int NS = Dims<MODE, 1>::NS;
 #pragma unroll
-    for (int k = 0; k < Dims<MODE, 1>::NS; ++k) st_out(&x[k * B + i], xs[k]);
+    for (int p = 0; p < NS / 2; ++p) st_out2d(&x[2 * (p * B + i)], xs[2 * p], xs[2 * p + 1]);
+    if constexpr (NS % 2) st_out(&x[(NS - 1) * B + i], xs[NS - 1]);
 }
 
 template <int MODE>
@@ -45,6 +53,53 @@ __device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double*
     } else {
 #pragma unroll
         for (int k = 0; k < NO; ++k) st_out(&obs[i * NO + k], (float)o[k]);
+    }
+}
+
+// Observation store through LDS (RCBF_OBS_STAGE=1): a full wave's 64 obs rows
+// are one contiguous (64*NO*4)-byte block; lanes write their rows into LDS,
+// then store the block as 16-byte chunks, chunk c by lane c%64 -- every
+// store instruction covers whole contiguous lines (cars: 3 dwordx4 instead of
+// 5 strided dwordx2).  Partial or unaligned waves take the per-lane path.
+#ifndef RCBF_OBS_STAGE
+#define RCBF_OBS_STAGE 1
+#endif
+template <int MODE>
+__device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_t B, const double* xs,
+                                                   const double* obs_cache, float* lds_wave) {
+    constexpr int NO = Dims<MODE, 1>::NO;
+    const int lane = threadIdx.x & 63;
+    const int64_t base = i - lane;
+    const bool full = (kEnvsPerWave == 64) && (base + 64 <= B) && ((reinterpret_cast<uintptr_t>(obs) & 15) == 0);
+    if (!full) {
+        store_obs32<MODE>(obs, i, xs, obs_cache);
+        return;
+    }
+    double o[NO];
+    if constexpr (MODE == RCBF_MODE_UNICYCLE && (kAblate & 8) == 0) {
+        if (obs_cache && obs_cache[3] != 0.0)
+            uni_obs_cs(xs, obs_cache[0], obs_cache[1], obs_cache[2], o);
+        else
+            env_obs<MODE>(xs, o);
+    } else {
+        env_obs<MODE>(xs, o);
+    }
+    if constexpr (NO % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < NO / 2; ++k)
+            *reinterpret_cast<float2*>(&lds_wave[lane * NO + 2 * k]) = make_float2((float)o[2 * k], (float)o[2 * k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NO; ++k) lds_wave[lane * NO + k] = (float)o[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    constexpr int CH = NO * 16;  // 16-byte chunks in the wave's block
+    const float4* src = reinterpret_cast<const float4*>(lds_wave);
+    float* dst = obs + base * NO;
+#pragma unroll
+    for (int j = 0; j < (CH + 63) / 64; ++j) {
+        const int c = j * 64 + lane;
+        if (CH % 64 == 0 || c < CH) st_out4(dst + 4 * c, src[c]);
     }
 }
 
@@ -141,11 +196,11 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B
     RCBF_STAMP(stamps, 0, false);
     double xs[D::NS];
     load_state<MODE>(x, B, i, xs);
-    double a = aux[i];
-    int st = step[i];
+    double a = ld_in(&aux[i]);
+    int st = ld_in(&step[i]);
     float us[D::NU], m[D::NS], s[D::NS], uf[D::NU];
 #pragma unroll
-    for (int c = 0; c < D::NU; ++c) us[c] = u_rl[i * D::NU + c];
+    for (int c = 0; c < D::NU; ++c) us[c] = ld_in(&u_rl[i * D::NU + c]);
 #pragma unroll
     for (int k = 0; k < D::NS; ++k) {
         m[k] = mu ? mu[i * D::NS + k] : 0.0f;
@@ -156,14 +211,26 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B
     int status;
     RCBF_STAMP(stamps, 1, true);
     double oc[4] = {0.0, 0.0, 0.0, 0.0};
+#if RCBF_EARLY_STORE
+    safe_step_one<SOLVER, MODE, K>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
+                                   seed, off, stamps, oc, u_out);
+#else
     safe_step_one<SOLVER, MODE, K>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
                                    seed, off, stamps, oc);
+#endif
     store_state<MODE>(x, B, i, xs);
     st_out(&aux[i], a);
     st_out(&step[i], st);
+#if RCBF_OBS_STAGE
+    __shared__ float obs_stage[kBlock / 64][64 * D::NO];
+    store_obs32_staged<MODE>(obs_out, i, B, xs, oc, obs_stage[threadIdx.x >> 6]);
+#else
     store_obs32<MODE>(obs_out, i, xs, oc);
+#endif
+#if !RCBF_EARLY_STORE
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
+#endif
     st_out(&reward[i], rew);
     st_out(&cost[i], cst);
     st_out(&done[i], (uint8_t)dn);
@@ -235,7 +302,7 @@ int rcbf_env_reset(const rcbf_params* prm, int64_t B, const uint8_t* mask, const
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !aux || !step) return RCBF_E_NULL;
-    if (obs_out && (((uintptr_t)obs_out) & 7)) return RCBF_E_BAD_SHAPE;
+    if ((obs_out && (((uintptr_t)obs_out) & 7)) || (((uintptr_t)x) & 15)) return RCBF_E_BAD_SHAPE;
     if (prm->mode == RCBF_MODE_SIMULATED_CARS)
         hipLaunchKernelGGL((k_env_reset<RCBF_MODE_SIMULATED_CARS>), dim3(grid_for_envs(B)), dim3(kBlock), 0, stream, *prm,
                            B, mask, noise, seed, env_offset, x, aux, step, episode, obs_out);
@@ -253,7 +320,7 @@ int rcbf_env_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !aux || !step || !action || !reward || !cost || !done) return RCBF_E_NULL;
-    if (obs_out && (((uintptr_t)obs_out) & 7)) return RCBF_E_BAD_SHAPE;
+    if ((obs_out && (((uintptr_t)obs_out) & 7)) || (((uintptr_t)x) & 15)) return RCBF_E_BAD_SHAPE;
     dim3 g(grid_for_envs(B)), b(kBlock);
 #define RCBF_ENV_L(MODE, A)                                                                                       \
     hipLaunchKernelGGL((k_env_step<MODE, A>), g, b, 0, stream, *prm, B, x, aux, step, episode, (const A*)action, \
@@ -281,7 +348,7 @@ int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, in
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !aux || !step || !u_rl || !obs_out || !u_out || !reward || !cost || !done) return RCBF_E_NULL;
-    if (((uintptr_t)obs_out) & 7) return RCBF_E_BAD_SHAPE;  // float2 row stores
+    if ((((uintptr_t)obs_out) & 7) || (((uintptr_t)x) & 15)) return RCBF_E_BAD_SHAPE;  // 8/16-B accesses
     RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0,
                                           stream, *prm, B, x, aux, step, episode, u_rl, mu, sigma, obs_out, u_out,
                                           reward, cost, done, goal_met, status_out, fail_flag, auto_reset, seed,
@@ -296,7 +363,7 @@ int rcbf_safe_rollout(const rcbf_params* prm, int64_t B, int32_t K, double* x, d
     if (B < 0 || K < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0 || K == 0) return 0;
     if (!x || !aux || !step || !u_rl || !reward_sum || !cost_sum || !n_done) return RCBF_E_NULL;
-    if (obs_out && (((uintptr_t)obs_out) & 7)) return RCBF_E_BAD_SHAPE;
+    if ((obs_out && (((uintptr_t)obs_out) & 7)) || (((uintptr_t)x) & 15)) return RCBF_E_BAD_SHAPE;
     RCBF_DISPATCH_MODE(prm, hipLaunchKernelGGL((k_safe_rollout<MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0,
                                                stream, *prm, B, K, x, aux, step, episode, u_rl, obs_out, reward_sum,
                                                cost_sum, n_done, fail_flag, seed, env_offset));

@@ -9,9 +9,9 @@
   dynamics_mode, kp/k_brake, hazards_*) on a B = 1 device env, so the
   reference's main.py loop runs unchanged.
 
-Per-env state in HBM, component-major (SoA) so every component access of a
-wavefront is contiguous: x (n_s, B) f64 = env.state (`.state` is the (B, n_s)
-view); aux (B,) f64 = env.t (cars) or env.last_goal_dist (unicycle); step (B,)
+Per-env state in HBM, component-pair-major (include/rcbf_hip.h) so every
+component-pair access of a wavefront is one contiguous 1 KiB dwordx4 access:
+x (n_s * B,) f64 holds env.state (`.state` is the (B, n_s) tensor); aux (B,) f64 = env.t (cars) or env.last_goal_dist (unicycle); step (B,)
 i32 = env.episode_step; episode (B,) i32 = reset counter keying the
 counter-based reset RNG (so the cars' N(0, 0.5) reset draw depends only on
 (seed, global env index, episode) and is identical however the envs are
@@ -90,6 +90,25 @@ class _EnvSpec:
             self.n_s, self.n_u, self.n_o = 3, 2, 7
 
 
+def pairs_to_rows(xf, n_s, B):
+    """(n_s*B,) component-pair-major buffer -> (B, n_s) rows."""
+    P = n_s // 2
+    rows = xf[:2 * P * B].view(P, B, 2).permute(1, 0, 2).reshape(B, 2 * P)
+    if n_s % 2:
+        rows = torch.cat([rows, xf[2 * P * B:].view(B, 1)], 1)
+    return rows
+
+
+def rows_to_pairs(rows):
+    """(B, n_s) rows -> (n_s*B,) component-pair-major buffer."""
+    B, n_s = rows.shape
+    P = n_s // 2
+    head = rows[:, :2 * P].reshape(B, P, 2).permute(1, 0, 2).reshape(-1)
+    if n_s % 2:
+        head = torch.cat([head, rows[:, n_s - 1].contiguous()])
+    return head.contiguous()
+
+
 class BatchedEnv:
     """B independent envs resident on one HIP device."""
 
@@ -105,7 +124,7 @@ class BatchedEnv:
         self.seed_value = int(seed)
         self.env_offset = int(env_offset)  # global index of env 0 (sharding)
         B, d = self.num_envs, self.device
-        self.x = torch.zeros(self.n_s, B, dtype=torch.float64, device=d)  # SoA
+        self.x = torch.zeros(self.n_s * B, dtype=torch.float64, device=d)  # component-pair-major
         self.aux = torch.zeros(B, dtype=torch.float64, device=d)
         self.step_count = torch.zeros(B, dtype=torch.int32, device=d)
         self.episode = torch.zeros(B, dtype=torch.int32, device=d)
@@ -117,16 +136,17 @@ class BatchedEnv:
 
     @property
     def state(self):
-        """(B, n_s) view of the SoA state."""
-        return self.x.t()
+        """(B, n_s) tensor of the env states (a copy out of the pair-major buffer)."""
+        return pairs_to_rows(self.x, self.n_s, self.num_envs)
 
     def state_numpy(self):
-        return self.x.t().cpu().numpy()
+        return self.state.cpu().numpy()
 
     def load_state(self, x=None, aux=None, step=None):
         """Overwrite the state of every env: x (B, n_s), aux (B,), step (B,)."""
         if x is not None:
-            self.x.copy_(torch.as_tensor(np.asarray(x), dtype=torch.float64, device=self.device).t())
+            rows = torch.as_tensor(np.asarray(x), dtype=torch.float64, device=self.device)
+            self.x.copy_(rows_to_pairs(rows.reshape(self.num_envs, self.n_s)))
         if aux is not None:
             self.aux.copy_(torch.as_tensor(np.asarray(aux), dtype=torch.float64, device=self.device))
         if step is not None:
@@ -255,11 +275,11 @@ class _SingleEnv(_EnvBase):
     # env.state / env.t / env.episode_step / env.last_goal_dist as numpy views
     @property
     def state(self):
-        return self._b.x[:, 0].cpu().numpy().copy()
+        return self._b.x.cpu().numpy().copy()  # B = 1: the buffer is the state row
 
     @state.setter
     def state(self, v):
-        self._b.x[:, 0] = torch.as_tensor(np.asarray(v, np.float64), device=self._b.device)
+        self._b.x.copy_(torch.as_tensor(np.asarray(v, np.float64).reshape(-1), device=self._b.device))
 
     @property
     def episode_step(self):

@@ -86,3 +86,25 @@ def test_layer_requires_device():
     from rcbf_amd.envs import BatchedSimulatedCarsEnv
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         BatchedSimulatedCarsEnv(4)
+
+
+def test_state_pair_layout_roundtrip():
+    """envs.pairs_to_rows / rows_to_pairs restate the device layout of
+    include/rcbf_hip.h: pair p of env i at x[2(pB+i)+j], odd last component
+    at x[(n_s-1)B+i]."""
+    import torch
+    from rcbf_amd.envs import pairs_to_rows, rows_to_pairs
+    for n_s, B in [(10, 7), (3, 5), (3, 1), (10, 1), (4, 64)]:
+        rows = torch.arange(B * n_s, dtype=torch.float64).reshape(B, n_s)
+        xf = rows_to_pairs(rows)
+        assert xf.shape == (n_s * B,)
+        for i in range(B):
+            for k in range(n_s):
+                if k < 2 * (n_s // 2):
+                    idx = 2 * ((k // 2) * B + i) + (k % 2)
+                else:
+                    idx = (n_s - 1) * B + i
+                assert xf[idx] == rows[i, k]
+        assert torch.equal(pairs_to_rows(xf, n_s, B), rows)
+        if B == 1:
+            assert torch.equal(xf, rows[0])
