@@ -17,7 +17,7 @@ constexpr int kBlock = RCBF_BLOCK;
 // Ablation switches for performance studies only (scripts/build_variants.sh
 // builds them into separate libraries; the product build uses 0):
 //   1 = no QP (u_qp = 0), 2 = no rows/normalise/QP, 4 = no env dynamics,
-//   8 = no observation maths
+//   8 = no observation maths, 16 = no auto-reset
 #ifndef RCBF_ABLATE
 #define RCBF_ABLATE 0
 #endif
@@ -349,7 +349,7 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
                                               float* uf, float& rew, float& cst, bool& dn, bool& gm, int& status,
                                               int auto_reset, uint64_t seed, int64_t off,
                                               unsigned long long* stamps = nullptr, double* obs_cache = nullptr,
-                                              float* u_out = nullptr) {
+                                              float* u_out = nullptr, bool ep_pre = false, uint32_t ep0 = 0) {
     using D = Dims<MODE, K>;
     float s32[D::NS];
     state_from_env<MODE>(xs, s32);
@@ -399,12 +399,35 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
         }
     }
     RCBF_STAMP(stamps, 5, false);
-    if (auto_reset && dn) {
-        uint32_t ep = episode ? episode[i] + 1u : 0u;
+    if (auto_reset && dn && (kAblate & 16) == 0) {
+        // ep_pre: the caller loaded episode[i] with the state (reset_foreseeable)
+        uint32_t ep = episode ? (ep_pre ? ep0 : episode[i]) + 1u : 0u;
         if (episode) episode[i] = ep;
         env_reset_one<MODE>(nullptr, i, seed, off, ep, xs, a, st);
-        if (obs_cache) obs_cache[3] = 0.0;
+        if (obs_cache) {
+            if constexpr (MODE == RCBF_MODE_UNICYCLE) {  // the reset state's obs inputs
+                obs_cache[0] = 1.0;                       // cos 0
+                obs_cache[1] = 0.0;                       // sin 0
+                obs_cache[2] = a;                         // goal distance of the reset state
+                obs_cache[3] = 1.0;
+            } else {
+                obs_cache[3] = 0.0;
+            }
+        }
     }
+}
+
+// Whether this env can finish its episode in this step, known before the
+// step: the time limit, or (unicycle) being within reach of the goal (a step
+// moves the robot by at most dt (|u0| + 0.1) = 0.022 < 0.2 and the goal test
+// is d <= 0.3).  Such envs load their episode counter together with the state
+// so the reset does not wait on a dependent load at the end of the step.
+template <int MODE>
+__device__ __forceinline__ bool reset_foreseeable(int st, double aux) {
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS)
+        return st + 1 >= 300;
+    else
+        return st + 1 >= 1000 || aux <= 0.5;
 }
 
 inline int check_prm(const rcbf_params* prm) {

@@ -201,6 +201,9 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B
     float us[D::NU], m[D::NS], s[D::NS], uf[D::NU];
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) us[c] = ld_in(&u_rl[i * D::NU + c]);
+    const bool ep_pre = episode && reset_foreseeable<MODE>(st, a);
+    uint32_t ep0 = 0;
+    if (ep_pre) ep0 = episode[i];
 #pragma unroll
     for (int k = 0; k < D::NS; ++k) {
         m[k] = mu ? mu[i * D::NS + k] : 0.0f;
@@ -211,13 +214,8 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B
     int status;
     RCBF_STAMP(stamps, 1, true);
     double oc[4] = {0.0, 0.0, 0.0, 0.0};
-#if RCBF_EARLY_STORE
     safe_step_one<SOLVER, MODE, K>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
-                                   seed, off, stamps, oc, u_out);
-#else
-    safe_step_one<SOLVER, MODE, K>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
-                                   seed, off, stamps, oc);
-#endif
+                                   seed, off, stamps, oc, RCBF_EARLY_STORE ? u_out : nullptr, ep_pre, ep0);
     store_state<MODE>(x, B, i, xs);
     st_out(&aux[i], a);
     st_out(&step[i], st);

@@ -144,13 +144,17 @@ class BatchedEnv:
 
     def load_state(self, x=None, aux=None, step=None):
         """Overwrite the state of every env: x (B, n_s), aux (B,), step (B,)."""
+        def dev(v, dt):
+            v = v if isinstance(v, torch.Tensor) else np.asarray(v)
+            return torch.as_tensor(v, device=self.device).to(dt)
+
         if x is not None:
-            rows = torch.as_tensor(np.asarray(x), dtype=torch.float64, device=self.device)
+            rows = dev(x, torch.float64)
             self.x.copy_(rows_to_pairs(rows.reshape(self.num_envs, self.n_s)))
         if aux is not None:
-            self.aux.copy_(torch.as_tensor(np.asarray(aux), dtype=torch.float64, device=self.device))
+            self.aux.copy_(dev(aux, torch.float64).reshape(-1))
         if step is not None:
-            self.step_count.copy_(torch.as_tensor(np.asarray(step), dtype=torch.int32, device=self.device))
+            self.step_count.copy_(dev(step, torch.int32).reshape(-1))
 
     def _rng_seed(self):
         return self.seed_value & 0xFFFFFFFFFFFFFFFF

@@ -34,6 +34,10 @@ for step in "$@"; do
               python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 ;;
     pmcv)   run pmcv 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc_valu" -o run -- \
               python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 ;;
+    pmcfu)  run pmcfu 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_u" -o run -- \
+              python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 --env Unicycle --hazards 3 ;;
+    pmcwu)  run pmcwu 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_u" -o run -- \
+              python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 --env Unicycle --hazards 3 ;;
     profu)  run profu 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profu" -o run -- \
               python3 bench.py --no-cpu-baseline --env Unicycle --hazards 3 ;;
     *) log "unknown step $step" ;;

@@ -24,10 +24,12 @@ uni = len(sys.argv) > 2 and sys.argv[2] == "unicycle"
 if uni:
     hz = np.array([[0., 0.], [-1., 1.], [-1., -1.]]) * 1.5
     env = BatchedUnicycleEnv(B, seed=3, hazards_locations=hz)
-    rng = np.random.default_rng(0)
-    env.load_state(np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1))
 else:
     env = BatchedSimulatedCarsEnv(B, seed=3)
+from bench import init_states  # noqa: E402  (SURVEY 8(d) start states, as the bench)
+gen = torch.Generator(device="cuda")
+gen.manual_seed(1000)
+init_states(env, gen, "Unicycle" if uni else "SimulatedCars")
 layer = CBFQPLayer(env, A(), gamma_b=20.0)
 o = env.make_outputs()
 nw = (B + 63) // 64
@@ -42,7 +44,7 @@ for rep in range(30):
     rc = lib.rcbf_safe_step(ctypes.byref(layer._prm), B, _lib.ptr(env.x), _lib.ptr(env.aux), _lib.ptr(env.step_count),
                             _lib.ptr(env.episode), _lib.ptr(u), None, None, _lib.ptr(env.obs), _lib.ptr(o["u"]),
                             _lib.ptr(o["reward"]), _lib.ptr(o["cost"]), _lib.ptr(o["done"]), None, _lib.ptr(st),
-                            None, 0 if uni else 1, 1, 0, _lib.stream_of(torch.device("cuda")))
+                            None, 1, 1, 0, _lib.stream_of(torch.device("cuda")))
     assert rc == 0
     torch.cuda.synchronize()
     if rep >= 10:

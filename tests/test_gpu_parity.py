@@ -331,6 +331,9 @@ def test_auto_reset_and_rng_sharding_invariance():
     assert nd == B and int(full.step_count.max().item()) == 0 and int(full.episode.min().item()) == 2
     v = full.state[:, 1].cpu().numpy() - 30.0
     assert 0.3 < v.std() < 0.7  # N(0, 0.5) reset draw
+    # the draw itself: 0.5 * Box-Muller(Philox4x32-10(seed, env, episode)), oracle restatement
+    ref = 0.5 * O.normal_draw(9, np.arange(B), 2)
+    assert np.max(np.abs(v - ref)) < 1e-5  # hardware fp32 log2/cos vs numpy fp32
 
 
 def test_large_batch_properties():

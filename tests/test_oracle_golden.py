@@ -134,3 +134,21 @@ def test_closed_loop_config1(golden):
         assert rel(z[:, :1], cl["u_safe"][k]) < 1e-8
         x, t, st, obs, r, c, dn = O.cars_step(x, t, st, un[None] + cl["u_safe"][k][None])
         assert np.array_equal(x[0], cl["state"][k + 1])
+
+
+def test_philox_known_answer():
+    """Philox4x32-10 known-answer vectors (Random123 kat_vectors, the
+    published test vectors of Salmon et al.): counter/key all zero and all
+    ones.  Pins the oracle restatement of the batched envs' reset RNG."""
+    c = O.philox4x32_10([np.uint64(0)] * 4, 0)
+    assert [int(v) for v in c] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    ff = np.uint64(0xFFFFFFFF)
+    c = O.philox4x32_10([ff] * 4, 0xFFFFFFFFFFFFFFFF)
+    assert [int(v) for v in c] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+
+
+def test_normal_draw_distribution():
+    z = O.normal_draw(1234, np.arange(200000), 1)
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
+    z2 = O.normal_draw(1234, np.arange(200000), 2)
+    assert abs(np.corrcoef(z, z2)[0, 1]) < 0.01
