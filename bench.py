@@ -270,6 +270,79 @@ def main():
         dist.destroy_process_group()
 
 
+def sac_update_safe_action(env, layer, dev):
+    """RCBF_SAC.get_safe_action on a replay batch as the SAC
+    update calls it (obs -> get_state -> prior -> CBF-QP layer, forward and
+    backward w.r.t. the policy action), B = 256 / 512 / 4096 (config 5).
+    kernel_us: rcbf_obs_safe_action + its backward captured in a hipGraph;
+    autograd_us: the Python surface (rcbf_amd.sac_cbf.get_safe_action +
+    .backward) eagerly, including the host fail-flag check."""
+    import ctypes
+    from rcbf_amd import _lib
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.sac_cbf import get_safe_action
+
+    class A:
+        cuda = True
+
+    lib = _lib.load()
+    dyn = DynamicsModel(env, A())
+    res = {}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(77)
+    for B in (256, 512, 4096):
+        obs = env.obs[:B].clone()
+        u = (torch.rand(B, env.n_u, device=dev, generator=gen) * 2 - 1).contiguous()
+        w = torch.randn(B, env.n_u, device=dev, generator=gen)
+        uo = torch.empty_like(u)
+        gu = torch.empty_like(u)
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        stream = torch.cuda.Stream(device=dev)
+        reps = 50
+
+        def launch():
+            s = _lib.stream_of(dev)
+            lib.rcbf_obs_safe_action(ctypes.byref(layer._prm), B, _lib.ptr(obs), _lib.ptr(u), None, None,
+                                     _lib.ptr(uo), None, _lib.ptr(flag), s)
+            lib.rcbf_obs_safe_action_backward(ctypes.byref(layer._prm), B, _lib.ptr(obs), _lib.ptr(u), None, None,
+                                              _lib.ptr(w), _lib.ptr(gu), s)
+
+        with torch.cuda.stream(stream):
+            launch()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for _ in range(reps):
+                launch()
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(4):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        k_us = e0.elapsed_time(e1) * 1e3 / (4 * reps)
+
+        def eager():
+            uu = u.clone().requires_grad_(True)
+            out = get_safe_action(layer, obs, uu, dyn)
+            (out * w).sum().backward()
+            return uu.grad
+
+        for _ in range(5):
+            eager()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 50
+        for _ in range(n):
+            eager()
+        torch.cuda.synchronize()
+        a_us = (time.perf_counter() - t0) * 1e6 / n
+        res[f"sac_safe_action_fwd_bwd_B{B}"] = {"kernel_us": round(k_us, 2), "autograd_us": round(a_us, 1)}
+    return res
+
+
 def extra_measurements(env, layer, dev, args):
     """Secondary numbers (not `value`): the K-step rollout kernel (state in
     registers across steps) and the fused step at a batch beyond the 256 MiB
@@ -287,6 +360,7 @@ def extra_measurements(env, layer, dev, args):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)
     out["rollout_K100_steps_per_s"] = round(env.num_envs * K / (ms * 1e-3), 1)
+    out.update(sac_update_safe_action(env, layer, dev))
     if args.env == "SimulatedCars":
         Bb = 4 * 1024 * 1024
         big = BatchedSimulatedCarsEnv(Bb, device=dev, seed=5)

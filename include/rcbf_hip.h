@@ -125,6 +125,22 @@ int rcbf_safe_action_backward(const rcbf_params* prm, int64_t B, const float* x,
                               const float* u_rl, const float* mu, const float* sigma,
                               const float* grad_u, float* grad_u_rl, hipStream_t stream);
 
+/* RCBF_SAC.get_safe_action (sac_cbf.py:218-238) with the prior disturbance
+ * model, as the SAC update calls it on replay batches (sac_cbf.py:133,149):
+ * DynamicsModel.get_state (dynamics.py:190-232) from the fp32 observation
+ * obs (B,n_o) in-kernel, then exactly rcbf_safe_action.  mu/sigma (B,n_s)
+ * [nullable: the MAX_STD prior of predict_disturbance, dynamics.py:381-384]. */
+int rcbf_obs_safe_action(const rcbf_params* prm, int64_t B, const float* obs,
+                         const float* u_rl, const float* mu, const float* sigma,
+                         float* u_out, int32_t* status_out, int32_t* fail_flag,
+                         hipStream_t stream);
+
+/* Backward of rcbf_obs_safe_action w.r.t. u_rl (the policy's action; obs,
+ * mean and sigma are detached in the reference, dynamics.py:211,362). */
+int rcbf_obs_safe_action_backward(const rcbf_params* prm, int64_t B, const float* obs,
+                                  const float* u_rl, const float* mu, const float* sigma,
+                                  const float* grad_u, float* grad_u_rl, hipStream_t stream);
+
 /* CascadeCBFLayer.get_u_safe (cbf_qp.py:29-53), fp64 batched: build ->
  * normalise -> exact QP.  Returns u_qp only (caller adds u_nom, no clamp). */
 int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom,

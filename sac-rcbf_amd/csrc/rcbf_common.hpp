@@ -322,21 +322,34 @@ __device__ __forceinline__ void env_obs(const double* xs, double* o) {
     }
 }
 
+// DynamicsModel.get_state (dynamics.py:190-232) on an fp32 observation row:
+// cars scale positions x100, velocities x30 (numpy fp32 in-place multiply:
+// one rounding of the exact product, which the fp64 product then cast
+// reproduces); unicycle theta = arctan2(sin, cos).  Result cast to fp32 like
+// to_tensor(state, obs.dtype).
+template <int MODE>
+__device__ __forceinline__ void state_from_obs32(const float* o, float* s32) {
+#pragma clang fp contract(off)
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) s32[k] = (float)((double)o[k] * ((k & 1) ? 30.0 : 100.0));
+    } else {
+        s32[0] = o[0];
+        s32[1] = o[1];
+        s32[2] = (float)atan2((double)o[3], (double)o[2]);
+    }
+}
+
 // state32 = get_state(float(obs(x)))   (dynamics.py:190-232, via the fp32
 // observation the policy sees: sac_cbf.py:61 then to_numpy/fp64/rescale/fp32)
 template <int MODE>
 __device__ __forceinline__ void state_from_env(const double* xs, float* s32) {
-#pragma clang fp contract(off)
     double o[Dims<MODE, 1>::NO];
     env_obs<MODE>(xs, o);
-    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+    float o32[Dims<MODE, 1>::NO];
 #pragma unroll
-        for (int k = 0; k < 10; ++k) s32[k] = (float)((double)(float)o[k] * ((k & 1) ? 30.0 : 100.0));
-    } else {
-        s32[0] = (float)o[0];
-        s32[1] = (float)o[1];
-        s32[2] = (float)atan2((double)(float)o[3], (double)(float)o[2]);
-    }
+    for (int k = 0; k < Dims<MODE, 1>::NO; ++k) o32[k] = (float)o[k];
+    state_from_obs32<MODE>(o32, s32);
 }
 
 // One fused safe step for one env (shared by k_safe_step and k_safe_rollout).

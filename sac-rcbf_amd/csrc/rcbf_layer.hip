@@ -90,13 +90,22 @@ __global__ void __launch_bounds__(kBlock) k_build_f64(rcbf_params prm, int64_t B
     }
 }
 
-template <int MODE, int K>
+// FROM_OBS: x is the (B, n_o) observation and the state comes from
+// DynamicsModel.get_state in-kernel (RCBF_SAC.get_safe_action, sac_cbf.py:218-238).
+template <int MODE, int K, bool FROM_OBS = false>
 __device__ __forceinline__ void load_layer_inputs(int64_t i, const float* x, const float* u, const float* mu,
                                                   const float* sigma, float* xs, float* us, float* m, float* s) {
     using D = Dims<MODE, K>;
+    if constexpr (FROM_OBS) {
+        constexpr int NO = Dims<MODE, 1>::NO;
+        float o[NO];
+#pragma unroll
+        for (int k = 0; k < NO; ++k) o[k] = x[i * NO + k];
+        state_from_obs32<MODE>(o, xs);
+    }
 #pragma unroll
     for (int k = 0; k < D::NS; ++k) {
-        xs[k] = x[i * D::NS + k];
+        if constexpr (!FROM_OBS) xs[k] = x[i * D::NS + k];
         m[k] = mu ? mu[i * D::NS + k] : 0.0f;
         s[k] = sigma ? sigma[i * D::NS + k] : prior_sigma<MODE>(k);
     }
@@ -104,7 +113,7 @@ __device__ __forceinline__ void load_layer_inputs(int64_t i, const float* x, con
     for (int c = 0; c < D::NU; ++c) us[c] = u[i * D::NU + c];
 }
 
-template <int SOLVER, int MODE, int K>
+template <int SOLVER, int MODE, int K, bool FROM_OBS = false>
 __global__ void __launch_bounds__(kBlock) k_safe_action(rcbf_params prm, int64_t B, const float* __restrict__ x,
                                                         const float* __restrict__ u, const float* __restrict__ mu,
                                                         const float* __restrict__ sigma, float* __restrict__ u_out,
@@ -113,7 +122,7 @@ __global__ void __launch_bounds__(kBlock) k_safe_action(rcbf_params prm, int64_t
     int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= B) return;
     float xs[D::NS], us[D::NU], m[D::NS], s[D::NS], uf[D::NU];
-    load_layer_inputs<MODE, K>(i, x, u, mu, sigma, xs, us, m, s);
+    load_layer_inputs<MODE, K, FROM_OBS>(i, x, u, mu, sigma, xs, us, m, s);
     LayerState<MODE, K> L;
     layer_forward<SOLVER, MODE, K>(prm, xs, us, m, s, uf, L);
 #pragma unroll
@@ -128,7 +137,7 @@ __global__ void __launch_bounds__(kBlock) k_safe_action(rcbf_params prm, int64_t
 // backward passes where lo <= v <= hi).  dh_r/du_c is closed form:
 //   CBF rows: dh/du = Lg (cars) or a_j (unicycle) = -G_raw[r][c];
 //   actuator rows (u_max - u, -u_min + u): -1 / +1.
-template <int SOLVER, int MODE, int K>
+template <int SOLVER, int MODE, int K, bool FROM_OBS = false>
 __global__ void __launch_bounds__(kBlock) k_safe_action_bwd(rcbf_params prm, int64_t B, const float* __restrict__ x,
                                                             const float* __restrict__ u, const float* __restrict__ mu,
                                                             const float* __restrict__ sigma,
@@ -139,7 +148,7 @@ __global__ void __launch_bounds__(kBlock) k_safe_action_bwd(rcbf_params prm, int
     int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= B) return;
     float xs[D::NS], us[NU], m[D::NS], s[D::NS], uf[NU];
-    load_layer_inputs<MODE, K>(i, x, u, mu, sigma, xs, us, m, s);
+    load_layer_inputs<MODE, K, FROM_OBS>(i, x, u, mu, sigma, xs, us, m, s);
     LayerState<MODE, K> L;
     layer_forward<SOLVER, MODE, K, true>(prm, xs, us, m, s, uf, L);
     double pd[N];
@@ -310,6 +319,30 @@ int rcbf_safe_action_backward(const rcbf_params* prm, int64_t B, const float* x,
     if (!x || !u_rl || !grad_u || !grad_u_rl) return RCBF_E_NULL;
     RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_action_bwd<SOLVER_, MODE_, K_>), dim3(grid_for(B)), dim3(kBlock),
                                           0, stream, *prm, B, x, u_rl, mu, sigma, grad_u, grad_u_rl));
+    return launch_status();
+}
+
+int rcbf_obs_safe_action(const rcbf_params* prm, int64_t B, const float* obs, const float* u_rl, const float* mu,
+                         const float* sigma, float* u_out, int32_t* status_out, int32_t* fail_flag,
+                         hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!obs || !u_rl || !u_out) return RCBF_E_NULL;
+    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_action<SOLVER_, MODE_, K_, true>), dim3(grid_for(B)), dim3(kBlock),
+                                          0, stream, *prm, B, obs, u_rl, mu, sigma, u_out, status_out, fail_flag));
+    return launch_status();
+}
+
+int rcbf_obs_safe_action_backward(const rcbf_params* prm, int64_t B, const float* obs, const float* u_rl,
+                                  const float* mu, const float* sigma, const float* grad_u, float* grad_u_rl,
+                                  hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!obs || !u_rl || !grad_u || !grad_u_rl) return RCBF_E_NULL;
+    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_action_bwd<SOLVER_, MODE_, K_, true>), dim3(grid_for(B)),
+                                          dim3(kBlock), 0, stream, *prm, B, obs, u_rl, mu, sigma, grad_u, grad_u_rl));
     return launch_status();
 }
 

@@ -61,6 +61,8 @@ SIGNATURES = {
     "rcbf_qp_solve": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "rcbf_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_obs_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_obs_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_cascade_u_safe": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_env_reset": [_PRM, _I64, _P, _P, _U64, _I64, _P, _P, _P, _P, _P, _P],
     "rcbf_env_step": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],

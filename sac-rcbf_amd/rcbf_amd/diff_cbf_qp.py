@@ -41,18 +41,19 @@ class _SafeAction(torch.autograd.Function):
     reference whose state/mean/sigma arrive detached (dynamics.py:211,362)."""
 
     @staticmethod
-    def forward(ctx, layer, x, u, mu, sigma):
+    def forward(ctx, layer, x, u, mu, sigma, from_obs=False):
         lib = _lib.load()
         B = x.shape[0]
         out = torch.empty_like(u)
         flag = torch.zeros(1, dtype=torch.int32, device=x.device)
-        rc = lib.rcbf_safe_action(ctypes.byref(layer._prm), B, _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu),
-                                  _lib.ptr(sigma), _lib.ptr(out), None, _lib.ptr(flag),
-                                  _lib.stream_of(x.device))
-        _lib.check(rc, "rcbf_safe_action")
+        fn = lib.rcbf_obs_safe_action if from_obs else lib.rcbf_safe_action
+        rc = fn(ctypes.byref(layer._prm), B, _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu), _lib.ptr(sigma),
+                _lib.ptr(out), None, _lib.ptr(flag), _lib.stream_of(x.device))
+        _lib.check(rc, "rcbf_obs_safe_action" if from_obs else "rcbf_safe_action")
         if layer.check_failures:
             _raise_if_failed(flag)
         ctx.layer = layer
+        ctx.from_obs = from_obs
         ctx.save_for_backward(x, u, mu, sigma)
         return out
 
@@ -62,11 +63,11 @@ class _SafeAction(torch.autograd.Function):
         lib = _lib.load()
         g = grad.contiguous().to(torch.float32)
         gu = torch.empty_like(u)
-        rc = lib.rcbf_safe_action_backward(ctypes.byref(ctx.layer._prm), x.shape[0], _lib.ptr(x), _lib.ptr(u),
-                                           _lib.ptr(mu), _lib.ptr(sigma), _lib.ptr(g), _lib.ptr(gu),
-                                           _lib.stream_of(x.device))
-        _lib.check(rc, "rcbf_safe_action_backward")
-        return None, None, gu, None, None
+        fn = lib.rcbf_obs_safe_action_backward if ctx.from_obs else lib.rcbf_safe_action_backward
+        rc = fn(ctypes.byref(ctx.layer._prm), x.shape[0], _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu), _lib.ptr(sigma),
+                _lib.ptr(g), _lib.ptr(gu), _lib.stream_of(x.device))
+        _lib.check(rc, "rcbf_obs_safe_action_backward" if ctx.from_obs else "rcbf_safe_action_backward")
+        return None, None, gu, None, None, None
 
 
 class CBFQPLayer:

@@ -86,6 +86,49 @@ def test_unicycle_layer_golden(golden, k, tag, solver):
     assert rel(uu.grad.cpu().numpy(), d[tag + "_grad_u"]) <= 1e-5
 
 
+@pytest.mark.parametrize("mode", ["SimulatedCars", "Unicycle"])
+@pytest.mark.parametrize("B", [256, 512])
+def test_sac_update_safe_action_from_obs(mode, B):
+    """RCBF_SAC.get_safe_action(obs, action, dynamics_model)
+    (sac_cbf.py:218-238) as the SAC update calls it on replay batches: the
+    fused obs-input kernel == get_state (oracle) -> prior -> CBFQPLayer, the
+    state-input kernel bit for bit, and its gradient w.r.t. the action ==
+    the oracle's implicit-KKT derivative."""
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.sac_cbf import get_safe_action
+    rng = np.random.default_rng(B)
+    if mode == "SimulatedCars":
+        x, _, _ = _cars_states(B, 21)
+        obs = O.cars_obs(x).astype(np.float32)
+        hz = None
+        env = _env(mode)
+    else:
+        hz = O.UNI["hazards"][:3]
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        obs = O.uni_obs(x).astype(np.float32)
+        env = _env(mode, hz)
+    layer = _layer(env, 20.0)
+    dyn = DynamicsModel(env, Args())
+    n_u = env.n_u
+    u = rng.uniform(-1, 1, (B, n_u)).astype(np.float32)
+    w = rng.normal(0, 1, (B, n_u)).astype(np.float32)
+    uu = dev(u).requires_grad_(True)
+    out = get_safe_action(layer, dev(obs), uu, dyn)
+    (out * dev(w)).sum().backward()
+    s32 = O.get_state_f32(mode, obs)
+    mu, sg = O.predict_disturbance_prior(mode, B)
+    mu, sg = mu.astype(np.float32), sg.astype(np.float32)
+    fin, _ = O.safe_action_diff(mode, s32, u, mu, sg, 20.0, hazards=hz)
+    assert rel(out.detach().cpu().numpy(), fin) <= 1e-5
+    g, _ = O.safe_action_diff_grad(mode, s32, u, mu, sg, 20.0, w, hazards=hz)
+    assert rel(uu.grad.cpu().numpy(), g) <= 1e-5
+    # same numbers as the state-input kernel on the oracle's get_state
+    u2 = dev(u).requires_grad_(True)
+    out2 = layer.get_safe_action(dev(s32), u2, dev(mu), dev(sg))
+    (out2 * dev(w)).sum().backward()
+    assert torch.equal(out.detach(), out2.detach()) and torch.equal(uu.grad, u2.grad)
+
+
 def test_solve_qp_and_cbf_layer_surface(golden):
     d = golden("cars_layer")
     layer = _layer(_env("SimulatedCars"), float(d["gamma_b"]))
