@@ -149,6 +149,43 @@ int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom,
                         hipStream_t stream);
 
 /* ---------------------------------------------------------------------- */
+/* GP disturbance posterior                              */
+/* ---------------------------------------------------------------------- */
+/* The fitted disturbance model of DynamicsModel (dynamics.py:296-340): one
+ * exact GP per state dimension i (ScaleKernel(RBF) + Gaussian likelihood,
+ * gp_model.py:12-27) on shared normalised training inputs.  Built on the
+ * host after each fit (rcbf_amd.gp); all arrays are device memory. */
+typedef struct rcbf_gp_model {
+    int32_t n_s;     /* GPs = state dims = input dims (3 or 10)                 */
+    int32_t N;       /* training points                                         */
+    int32_t N_pad;   /* N rounded up to a multiple of 32 (padding rows: Rt = 0)  */
+    int32_t r;       /* rank of the variance factor (r = N: exact posterior)     */
+    int32_t C_pad;   /* columns of Rt per GP: multiple of 128, >= r + 1          */
+    int32_t _pad;
+    const float* xt;       /* (n_s, N_pad, n_s): train_x / (std + 1e-8) / (sqrt2 l_i) */
+    const float* tn2;      /* (n_s, N_pad): squared norms of the xt rows             */
+    const float* Rt;       /* (n_s, N_pad, C_pad): [R_i | alpha_i | 0], R R^T = (K+nI)^-1 */
+    const double* x_std;   /* (n_s,): train_x std; queries are x / x_std (no +1e-8,
+                              dynamics.py:376)                                       */
+    const float* inv_sl;   /* (n_s,): 1 / (sqrt(2) l_i)                              */
+    const float* outscale; /* (n_s,): s_i                                            */
+    const float* noise;    /* (n_s,): likelihood noise n_i                           */
+    const float* y_scale;  /* (n_s,): train_y std + 1e-8 (dynamics.py:379-380)      */
+} rcbf_gp_model;
+
+/* Floats of workspace rcbf_gp_predict needs for B queries. */
+int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B);
+
+/* DynamicsModel.predict_disturbance(test_x) with fitted GPs (dynamics.py:
+ * 342-390, gp_model.py:86-114): x (B, n_s) f32 states -> mean (B, n_s) and
+ * std (B, n_s) f32, std = sqrt(latent variance + noise) (the likelihood's
+ * predictive variance), both rescaled by y_scale.  Exact GP posterior when
+ * r = N (gpytorch's LOVE approximates this variance).  Two launches: the
+ * k(x, X) [R | alpha] GEMM on the fp32 MFMA, then a per-row finish. */
+int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out,
+                    float* std_out, float* workspace, hipStream_t stream);
+
+/* ---------------------------------------------------------------------- */
 /* Environments (batched, device-resident, fp64 state like the numpy envs) */
 /* ---------------------------------------------------------------------- */
 /* Per-env state, COMPONENT-PAIR-MAJOR:  x (n_s * B) f64, 16-byte aligned;

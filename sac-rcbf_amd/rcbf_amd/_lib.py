@@ -55,6 +55,18 @@ _I32 = ctypes.c_int32
 _U64 = ctypes.c_uint64
 _PRM = ctypes.POINTER(RcbfParams)
 
+
+class RcbfGpModel(ctypes.Structure):
+    """include/rcbf_hip.h rcbf_gp_model (device pointers as integers)."""
+    _fields_ = [("n_s", ctypes.c_int32), ("N", ctypes.c_int32), ("N_pad", ctypes.c_int32), ("r", ctypes.c_int32),
+                ("C_pad", ctypes.c_int32), ("_pad", ctypes.c_int32),
+                ("xt", ctypes.c_void_p), ("tn2", ctypes.c_void_p), ("Rt", ctypes.c_void_p),
+                ("x_std", ctypes.c_void_p), ("inv_sl", ctypes.c_void_p), ("outscale", ctypes.c_void_p),
+                ("noise", ctypes.c_void_p), ("y_scale", ctypes.c_void_p)]
+
+
+_GPM = ctypes.POINTER(RcbfGpModel)
+
 SIGNATURES = {
     "rcbf_build": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_build_f64": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
@@ -62,6 +74,8 @@ SIGNATURES = {
     "rcbf_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_obs_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_gp_workspace_floats": [_GPM, _I64],
+    "rcbf_gp_predict": [_GPM, _I64, _P, _P, _P, _P, _P],
     "rcbf_obs_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_cascade_u_safe": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_env_reset": [_PRM, _I64, _P, _P, _U64, _I64, _P, _P, _P, _P, _P, _P],
@@ -95,6 +109,7 @@ def load():
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int32
     lib.rcbf_version.restype = ctypes.c_char_p
+    lib.rcbf_gp_workspace_floats.restype = ctypes.c_int64
     if lib.rcbf_abi_version() != ABI_VERSION or lib.rcbf_params_size() != ctypes.sizeof(RcbfParams):
         raise RuntimeError("librcbf_hip.so ABI mismatch (rebuild with `python __graft_entry__.py build`)")
     _lib = lib

@@ -1,11 +1,10 @@
 """Dynamics-model glue on the hot path (rcbf_sac/dynamics.py).
 
-Only the pieces the safe step uses are here: DYNAMICS_MODE / MAX_STD
-(dynamics.py:22-24), get_state / get_obs (:190-261), the zero-mean MAX_STD
-prior of predict_disturbance (:381-384) and the model prior of
-predict_next_state (:60-105, :125-188).  GP learning (:263-340, gp_model.py)
-is out of scope (SURVEY.md section 8f ranks it "next"): a model with GP
-estimators attached raises instead of silently using the prior.
+DYNAMICS_MODE / MAX_STD (dynamics.py:22-24), get_state / get_obs
+(:190-261), predict_disturbance (:342-390) with the zero-mean MAX_STD prior
+or, once fitted, the GP posterior on the device (rcbf_amd.gp, the
+rcbf_gp_predict kernel), predict_next_state (:60-105) and the disturbance
+history + GP fit (append_transition / fit_gp_model, :263-340).
 
 Inside the fused step (rcbf_safe_step) get_state and the prior run in-kernel;
 this module serves the un-fused API: torch device tensors stay on device (no
@@ -21,7 +20,8 @@ MAX_STD = {"Unicycle": [2e-1, 2e-1, 2e-1], "SimulatedCars": [0, 0.2, 0, 0.2, 0, 
 
 
 class DynamicsModel:
-    """Prior-only DynamicsModel with the reference's constructor and methods."""
+    """DynamicsModel with the reference's constructor and methods; the GP
+    disturbance estimators are one rcbf_amd.gp.GPDisturbanceModel on the device."""
 
     def __init__(self, env, args):
         self.env = env
@@ -31,9 +31,46 @@ class DynamicsModel:
         self.n_u = DYNAMICS_MODE[env.dynamics_mode]["n_u"]
         self.disturb_estimators = None
         self.max_history_count = getattr(args, "gp_model_size", 2000)
+        self.disturbance_history = {"state": np.zeros((self.max_history_count, self.n_s)),
+                                    "disturbance": np.zeros((self.max_history_count, self.n_s))}
+        self.history_counter = 0
+        self.train_x = None
+        self.train_y = None
+        self.gp_rank = getattr(args, "gp_rank", None)  # None: exact posterior variance
         if hasattr(args, "l_p"):
             self.l_p = args.l_p
         self.device = torch.device("cuda" if getattr(args, "cuda", False) else "cpu")
+
+    # -- disturbance history and GP fit (dynamics.py:263-340) ----------------
+    def append_transition(self, state_batch, u_batch, next_state_batch, t_batch=None):
+        x = np.asarray(state_batch, np.float64)
+        expand = x.ndim == 1
+        x = np.atleast_2d(x)
+        nxt = np.atleast_2d(np.asarray(next_state_batch, np.float64))
+        u = np.atleast_2d(np.asarray(u_batch, np.float64))
+        t = None if t_batch is None else np.asarray(t_batch, np.float64)
+        if expand and t is not None:
+            t = t.reshape(1)
+        disturbance = (nxt - x - self.env.dt * self._f_plus_gu(x, u, t)) / self.env.dt
+        for i in range(x.shape[0]):
+            self.disturbance_history["state"][self.history_counter % self.max_history_count] = x[i]
+            self.disturbance_history["disturbance"][self.history_counter % self.max_history_count] = disturbance[i]
+            self.history_counter += 1
+            if self.history_counter % (self.max_history_count / 10) == 0:
+                self.fit_gp_model()
+
+    def fit_gp_model(self, training_iter=70):
+        from . import gp
+        if self.history_counter < self.max_history_count:
+            train_x = self.disturbance_history["state"][:self.history_counter]
+            train_y = self.disturbance_history["disturbance"][:self.history_counter]
+        else:
+            train_x = self.disturbance_history["state"]
+            train_y = self.disturbance_history["disturbance"]
+        self.disturb_estimators = gp.fit(train_x, train_y, MAX_STD[self.env.dynamics_mode], training_iter,
+                                         rank=self.gp_rank)
+        self.train_x = np.array(train_x, copy=True)
+        self.train_y = np.array(train_y, copy=True)
 
     # -- obs <-> state (dynamics.py:190-261) -------------------------------
     def get_state(self, obs):
@@ -71,7 +108,17 @@ class DynamicsModel:
     # -- disturbance prior (dynamics.py:342-390) ----------------------------
     def predict_disturbance(self, test_x):
         if self.disturb_estimators:
-            raise NotImplementedError("GP disturbance posterior is out of scope (SURVEY 8f row 1)")
+            gpm = self.disturb_estimators
+            if torch.is_tensor(test_x):
+                x = test_x.unsqueeze(0) if test_x.dim() == 1 else test_x
+                mean, std = gpm.predict(x.to(torch.float32))
+                mean, std = mean.to(test_x.dtype).to(test_x.device), std.to(test_x.dtype).to(test_x.device)
+                return (mean[0], std[0]) if test_x.dim() == 1 else (mean, std)
+            x = np.asarray(test_x, np.float64)
+            x2 = np.atleast_2d(x)
+            mean, std = gpm.predict(torch.as_tensor(x2, dtype=torch.float32))
+            mean, std = mean.double().cpu().numpy(), std.double().cpu().numpy()
+            return (mean[0], std[0]) if x.ndim == 1 else (mean, std)
         std = MAX_STD[self.env.dynamics_mode]
         if torch.is_tensor(test_x):
             mean = torch.zeros_like(test_x)
@@ -85,13 +132,25 @@ class DynamicsModel:
 
     # -- model prior step (dynamics.py:60-105, 125-188) ---------------------
     def predict_next_state(self, state_batch, u_batch, t_batch=None, use_gps=True):
-        if use_gps and self.disturb_estimators:
-            raise NotImplementedError("GP disturbance posterior is out of scope (SURVEY 8f row 1)")
         x = np.asarray(state_batch, np.float64)
         expand = x.ndim == 1
         x = np.atleast_2d(x)
         u = np.atleast_2d(np.asarray(u_batch, np.float64))
         dt = self.env.dt
+        nxt = x + dt * self._f_plus_gu(x, u, t_batch)
+        if use_gps:
+            mean, std = self.predict_disturbance(x)
+            nxt = nxt + dt * mean
+        else:
+            std = np.zeros(x.shape)
+        if expand:
+            nxt, std = nxt[0], std[0]
+        if t_batch is not None:
+            return nxt, dt * std, t_batch + dt
+        return nxt, dt * std, t_batch
+
+    def _f_plus_gu(self, x, u, t_batch):
+        """f(x) + g(x) u of the model prior (dynamics.py:125-188)."""
         if self.env.dynamics_mode == "Unicycle":
             f = np.zeros_like(x)
             gu = np.stack([np.cos(x[:, 2]) * u[:, 0], np.sin(x[:, 2]) * u[:, 0], u[:, 1]], axis=1)
@@ -110,10 +169,4 @@ class DynamicsModel:
             f[:, 1::2] = acc
             gu = np.zeros_like(x)
             gu[:, 7] = 50.0 * u[:, 0]
-        nxt = x + dt * (f + gu)
-        std = np.zeros(x.shape)
-        if expand:
-            nxt, std = nxt[0], std[0]
-        if t_batch is not None:
-            return nxt, dt * std, t_batch + dt
-        return nxt, dt * std, t_batch
+        return f + gu

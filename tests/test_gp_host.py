@@ -1,0 +1,101 @@
+"""CPU tests of the GP disturbance model host side and of
+the un-fused DynamicsModel glue: the hyperparameter fit (rcbf_amd.gp, torch)
+against the numpy oracle restatement of gpytorch's ExactGP training, and the
+device layout rcbf_gp_predict consumes ([R | alpha] factors, scaled inputs)
+evaluated here in fp64 against the oracle's exact posterior.  Parity against
+gpytorch itself is unpinned (gpytorch is not installed)."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+
+def _data(rng, N, n_s, smooth=True):
+    tx = rng.normal(0, 1, (N, n_s)) * rng.uniform(0.5, 2.0, n_s)
+    ty = 0.1 * np.sin(tx @ rng.normal(0, 1, (n_s, n_s))) + rng.normal(0, 0.05, (N, n_s))
+    return tx, ty
+
+
+def test_hyperparameter_fit_matches_oracle():
+    from rcbf_amd import gp
+    rng = np.random.default_rng(0)
+    tx, ty = _data(rng, 200, 3)
+    h_o = O.gp_fit(tx, ty, [0.2, 0.2, 0.2], training_iter=70)
+    xn = torch.as_tensor(tx / (tx.std(0) + 1e-8), dtype=torch.float32).double()
+    yn = torch.as_tensor(ty / (ty.std(0) + 1e-8), dtype=torch.float32).double()
+    for i in range(3):
+        h_p = gp.train_hyperparameters(xn, yn[:, i], 0.2, training_iter=70)
+        assert np.allclose(h_p, h_o[i], rtol=1e-9, atol=0)
+        # the reference's priors pin the lengthscale and outputscale near their means;
+        # the likelihood noise is what the 70 Adam steps move
+        assert abs(h_p[0] - 1e5) < 1.0 and abs(h_p[1] - 0.2) < 0.01 and h_p[2] > 0.7
+
+
+@pytest.mark.parametrize("rank", [None, 16])
+@pytest.mark.parametrize("n_s,N", [(3, 100), (10, 70)])
+def test_device_layout_reproduces_exact_posterior(n_s, N, rank):
+    """Q = k(x, X) Rt with the scaled inputs, as k_gp_qform computes it."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(n_s + N)
+    tx, ty = _data(rng, N, n_s)
+    hyper = [(rng.uniform(0.8, 2.5), rng.uniform(0.05, 0.5), rng.uniform(0.01, 0.2)) for _ in range(n_s)]
+    m = gp.GPDisturbanceModel(tx, ty, hyper, device="cpu", rank=rank)
+    q = rng.normal(0, 1, (33, n_s)) * tx.std(0)
+    xq = (q / tx.std(0)).astype(np.float32).astype(np.float64)
+    mean = np.zeros_like(xq)
+    std = np.zeros_like(xq)
+    Rt = m.Rt.double().numpy()
+    for i in range(n_s):
+        xs = xq * float(m.inv_sl[i])
+        xt = m.xt[i].double().numpy()
+        d2 = np.maximum((xs * xs).sum(1)[:, None] + m.tn2[i].double().numpy()[None] - 2 * xs @ xt.T, 0.0)
+        Ks = float(m.outscale[i]) * np.exp(-d2)
+        Q = Ks @ Rt[i]
+        lat = np.maximum(float(m.outscale[i]) - (Q[:, :m.r] ** 2).sum(1), 0.0)
+        mean[:, i] = Q[:, m.r] * float(m.y_scale[i])
+        std[:, i] = np.sqrt(lat + float(m.noise[i])) * float(m.y_scale[i])
+    mo, so = O.gp_predict(q, tx, ty, hyper, rank=rank)
+    assert np.max(np.abs(mean - mo)) <= 1e-5 * np.max(np.abs(mo)) + 1e-7
+    assert np.max(np.abs(std - so) / so) <= 1e-5
+
+
+def _dyn(mode):
+    from rcbf_amd.dynamics import DynamicsModel
+    env = types.SimpleNamespace(dynamics_mode=mode, dt=0.02)
+    return DynamicsModel(env, types.SimpleNamespace(cuda=False, gp_model_size=100))
+
+
+def test_dynamics_model_glue_vs_golden(golden):
+    """rcbf_amd.dynamics on the reference's own dynamics.py outputs."""
+    d = golden("dynamics")
+    for nm, mode in (("cars", "SimulatedCars"), ("uni", "Unicycle")):
+        dm = _dyn(mode)
+        assert np.array_equal(dm.get_state(d[nm + "_obs"]), d[nm + "_state_np"])
+        st = dm.get_state(torch.as_tensor(d[nm + "_obs32"]))
+        assert np.array_equal(st.numpy(), d[nm + "_state_t"])
+        m, s = dm.predict_disturbance(torch.as_tensor(d[nm + "_state_t"]))
+        assert np.array_equal(m.numpy(), d[nm + "_mean"]) and np.array_equal(s.numpy(), d[nm + "_sigma"])
+        nx, nstd, _ = dm.predict_next_state(d[nm + "_state_np"], d[nm + "_u"], d.get(nm + "_t"), use_gps=False)
+        assert np.array_equal(nx, d[nm + "_next"]) and not nstd.any()
+        # use_gps with no GP fitted: prior mean 0, std = dt * MAX_STD (dynamics.py:90-95)
+        nx2, nstd2, _ = dm.predict_next_state(d[nm + "_state_np"], d[nm + "_u"], d.get(nm + "_t"))
+        assert np.array_equal(nx2, d[nm + "_next"])
+        assert np.allclose(nstd2, 0.02 * np.asarray(O.MAX_STD[mode])[None])
+
+
+def test_append_transition_disturbance():
+    """dynamics.py:263-294: d = (x' - x - dt (f + g u)) / dt into a ring of
+    gp_model_size; a fit is triggered every gp_model_size / 10 points."""
+    dm = _dyn("Unicycle")
+    calls = []
+    dm.fit_gp_model = lambda *a, **k: calls.append(dm.history_counter)
+    rng = np.random.default_rng(3)
+    x = rng.normal(0, 1, (25, 3)); u = rng.uniform(-1, 1, (25, 2)); d_true = rng.normal(0, 0.1, (25, 3))
+    nx = O.predict_next_state_prior("Unicycle", x, u) + 0.02 * d_true
+    dm.append_transition(x, u, nx)
+    assert calls == [10, 20] and dm.history_counter == 25
+    assert np.allclose(dm.disturbance_history["disturbance"][:25], d_true, atol=1e-12)
+    assert np.array_equal(dm.disturbance_history["state"][:25], x)
