@@ -186,6 +186,32 @@ int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* me
                     float* std_out, float* workspace, hipStream_t stream);
 
 /* ---------------------------------------------------------------------- */
+/* Model-based rollouts and the device replay buffer  */
+/* ---------------------------------------------------------------------- */
+/* One k-step of generate_model_rollouts (rcbf_sac/generate_rollouts.py:24-77)
+ * on B replay transitions, fp64: state = get_state(obs); mu = model prior
+ * x + dt (f + g a) + dt * mean; next_state = mu + dt * std * z; next_obs =
+ * get_obs(next_state) (+ compass, exp(-dist) for the unicycle); reward, mask
+ * (= not done), next_t = t + dt.  obs (B,n_o) f64, act (B,n_u) f64, t (B,) f64
+ * [nullable for the unicycle]; mean/std (B,n_s) f32 [nullable: the MAX_STD
+ * prior]; z (B,n_s) f64 N(0,1) draws [nullable: Philox4x32-10 keyed by
+ * (seed, row, counter)]. */
+int rcbf_model_step(const rcbf_params* prm, int64_t B, const double* obs, const double* act,
+                    const double* t, const float* mean, const float* std, const double* z,
+                    uint64_t seed, uint64_t counter, double* next_obs, double* reward,
+                    double* mask, double* next_t, hipStream_t stream);
+
+/* ReplayMemory.batch_push (replay_memory.py:23-29) as one launch: n records
+ * of W f64 (state, action, reward, next_state, mask, t, next_t packed) into
+ * the ring of `cap` records starting at record `pos` (wrapping). */
+int rcbf_ring_scatter_f64(double* ring, int64_t cap, int64_t W, int64_t pos,
+                          const double* src, int64_t n, hipStream_t stream);
+
+/* ReplayMemory.sample (replay_memory.py:31-35) gather: dst[r] = ring[idx[r]]. */
+int rcbf_gather_rows_f64(double* dst, const double* ring, int64_t W, const int64_t* idx,
+                         int64_t n, hipStream_t stream);
+
+/* ---------------------------------------------------------------------- */
 /* Environments (batched, device-resident, fp64 state like the numpy envs) */
 /* ---------------------------------------------------------------------- */
 /* Per-env state, COMPONENT-PAIR-MAJOR:  x (n_s * B) f64, 16-byte aligned;

@@ -1,0 +1,216 @@
+// rcbf_model.hip -- model-based rollout step and the
+// device replay buffer's ring scatter / row gather (8f row 4) + C-ABI.
+//
+// rcbf_model_step restates one k-step of generate_model_rollouts
+// (rcbf_sac/generate_rollouts.py:24-77) for a batch of replay transitions:
+//   state = get_state(obs); (mu, std) = predict_next_state(state, a, t)
+//   (model prior + dt * disturbance mean, dt * disturbance std);
+//   next_state = mu + std * z; next_obs = get_obs(next_state) (+ compass and
+//   exp(-dist) for the unicycle); reward, done -> mask; next_t = t + dt.
+// All fp64 like the reference's numpy, with FMA contraction off so the
+// products round as numpy's do.
+#include "rcbf_common.hpp"
+
+using namespace rcbf;
+
+namespace {
+
+// get_state (dynamics.py:190-232), numpy fp64 path
+template <int MODE>
+__device__ __forceinline__ void model_state_from_obs(const double* o, double* xs) {
+#pragma clang fp contract(off)
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) xs[k] = o[k] * ((k & 1) ? 30.0 : 100.0);
+    } else {
+        xs[0] = o[0];
+        xs[1] = o[1];
+        xs[2] = atan2(o[3], o[2]);
+    }
+}
+
+// x + dt (f(x) + g(x) u) of the model prior (dynamics.py:60-105, 125-188)
+template <int MODE>
+__device__ __forceinline__ void model_prior_next(const double* xs, const double* u, double t, double* nx) {
+#pragma clang fp contract(off)
+    const double dt = 0.02;
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+        double pos[5], vel[5], acc[5];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            pos[c] = xs[2 * c];
+            vel[c] = xs[2 * c + 1];
+        }
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            double vdes = 30.0;
+            if (c == 0) vdes -= 10.0 * sin(0.2 * t);
+            acc[c] = 4.0 * (vdes - vel[c]);
+        }
+        const double d01 = pos[0] - pos[1], d12 = pos[1] - pos[2], d24 = pos[2] - pos[4];
+        acc[1] -= 20.0 * d01 * (d01 < 6.0 ? 1.0 : 0.0);
+        acc[2] -= 20.0 * d12 * (d12 < 6.0 ? 1.0 : 0.0);
+        acc[3] = 0.0;
+        acc[4] -= 20.0 * d24 * (d24 < 13.0 ? 1.0 : 0.0);
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            nx[2 * c] = xs[2 * c] + dt * (vel[c] + 0.0);
+            nx[2 * c + 1] = xs[2 * c + 1] + dt * (acc[c] + (c == 3 ? 50.0 * u[0] : 0.0));
+        }
+    } else {
+        double s, c;
+        sincos(xs[2], &s, &c);
+        nx[0] = xs[0] + dt * (0.0 + c * u[0]);
+        nx[1] = xs[1] + dt * (0.0 + s * u[0]);
+        nx[2] = xs[2] + dt * (0.0 + u[1]);
+    }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) k_model_step(rcbf_params prm, int64_t B, const double* __restrict__ obs,
+                                                       const double* __restrict__ act, const double* __restrict__ t,
+                                                       const float* __restrict__ mean, const float* __restrict__ stdv,
+                                                       const double* __restrict__ z, uint64_t seed, uint64_t counter,
+                                                       double* __restrict__ next_obs, double* __restrict__ reward,
+                                                       double* __restrict__ mask, double* __restrict__ next_t) {
+#pragma clang fp contract(off)
+    using D = Dims<MODE, 1>;
+    constexpr int NS = D::NS, NO = D::NO, NU = D::NU;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    const double dt = 0.02;
+    double o[NO], xs[NS], u[NU], nx[NS];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) o[k] = obs[i * NO + k];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) u[c] = act[i * NU + c];
+    const double ti = t ? t[i] : 0.0;
+    model_state_from_obs<MODE>(o, xs);
+    model_prior_next<MODE>(xs, u, ti, nx);
+    // disturbance: GP (mean, std) or the zero-mean MAX_STD prior (dynamics.py:381-384)
+    double zz[NS];
+    if (z) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) zz[k] = z[i * NS + k];
+    } else {  // N(0,1) pairs from Philox4x32-10 keyed by (seed, row, counter, pair)
+#pragma unroll
+        for (int p = 0; p < (NS + 1) / 2; ++p) {
+            uint32_t cc[4] = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), (uint32_t)counter, (uint32_t)p};
+            philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
+            const double u1 = ((double)((((uint64_t)cc[0] << 21) ^ cc[1]) & ((1ull << 53) - 1)) + 1.0) *
+                              (1.0 / 9007199254740992.0);
+            const double u2 = (double)((((uint64_t)cc[2] << 21) ^ cc[3]) & ((1ull << 53) - 1)) *
+                              (1.0 / 9007199254740992.0);
+            const double r = sqrt(-2.0 * log(u1));
+            double sn, cs;
+            sincospi(2.0 * u2, &sn, &cs);
+            zz[2 * p] = r * cs;
+            if (2 * p + 1 < NS) zz[2 * p + 1] = r * sn;
+        }
+    }
+    double ns[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const double m = mean ? (double)mean[i * NS + k] : 0.0;
+        // MAX_STD as numpy fp64 (dynamics.py:24,381-384)
+        const double prior = (MODE == RCBF_MODE_UNICYCLE || (k & 1)) ? 0.2 : 0.0;
+        const double sd = stdv ? (double)stdv[i * NS + k] : prior;
+        const double mu = nx[k] + dt * m;      // next_state_batch += dt * pred_mean
+        ns[k] = mu + (dt * sd) * zz[k];        // np.random.normal(mu, dt * pred_std)
+    }
+    double r, msk;
+    const double tn = ti + dt;
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) next_obs[i * NO + k] = ns[k] / ((k & 1) ? 30.0 : 100.0);
+        r = -5.0 * fabs(u[0] * u[0]) / 300.0;     // generate_rollouts.py:62
+        msk = (tn >= 300.0 * 0.02) ? 0.0 : 1.0;   // :65-66
+    } else {
+        double s, c;
+        sincos(ns[2], &s, &c);
+        const double g0 = 2.5 - ns[0], g1 = 2.5 - ns[1];
+        const double d = sqrt(g0 * g0 + g1 * g1);
+        double c0 = g0 * c + g1 * s;       // goal_rel @ R(theta)  (:41)
+        double c1 = g0 * (-s) + g1 * c;
+        const double nrm = sqrt(c0 * c0 + c1 * c1) + 0.001;
+        c0 = c0 / nrm;
+        c1 = c1 / nrm;
+        double* nw = &next_obs[i * NO];
+        nw[0] = ns[0];
+        nw[1] = ns[1];
+        nw[2] = c;
+        nw[3] = s;
+        nw[4] = c0;
+        nw[5] = c1;
+        nw[6] = exp(-d);
+        const double dprev = -log(o[NO - 1]);
+        const bool goal = d <= 0.3;
+        r = (dprev - d) * 1.0 + (goal ? 1.0 : 0.0);  // :47
+        r = r + 1.0 * (goal ? 1.0 : 0.0);          // :51, the goal bonus counted twice
+        msk = goal ? 0.0 : 1.0;
+    }
+    reward[i] = r;
+    mask[i] = msk;
+    if (next_t) next_t[i] = tn;
+}
+
+// Replay ring (rcbf_sac/replay_memory.py:12-32): records are rows of W f64.
+__global__ void __launch_bounds__(256) k_ring_scatter(double* __restrict__ ring, int64_t cap, int64_t W, int64_t pos,
+                                                      const double* __restrict__ src, int64_t n) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n * W) return;
+    const int64_t r = e / W, c = e - r * W;
+    ring[((pos + r) % cap) * W + c] = src[e];
+}
+
+__global__ void __launch_bounds__(256) k_gather_rows(double* __restrict__ dst, const double* __restrict__ ring,
+                                                     int64_t W, const int64_t* __restrict__ idx, int64_t n) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n * W) return;
+    const int64_t r = e / W, c = e - r * W;
+    dst[e] = ring[idx[r] * W + c];
+}
+
+}  // namespace
+
+extern "C" {
+
+int rcbf_model_step(const rcbf_params* prm, int64_t B, const double* obs, const double* act, const double* t,
+                    const float* mean, const float* stdv, const double* z, uint64_t seed, uint64_t counter,
+                    double* next_obs, double* reward, double* mask, double* next_t, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!obs || !act || !next_obs || !reward || !mask) return RCBF_E_NULL;
+    if (prm->mode == RCBF_MODE_SIMULATED_CARS && !t) return RCBF_E_NULL;  // cars dynamics need t
+    dim3 g(grid_for(B)), b(kBlock);
+    if (prm->mode == RCBF_MODE_SIMULATED_CARS)
+        hipLaunchKernelGGL((k_model_step<RCBF_MODE_SIMULATED_CARS>), g, b, 0, stream, *prm, B, obs, act, t, mean, stdv,
+                           z, seed, counter, next_obs, reward, mask, next_t);
+    else
+        hipLaunchKernelGGL((k_model_step<RCBF_MODE_UNICYCLE>), g, b, 0, stream, *prm, B, obs, act, t, mean, stdv, z,
+                           seed, counter, next_obs, reward, mask, next_t);
+    return launch_status();
+}
+
+int rcbf_ring_scatter_f64(double* ring, int64_t cap, int64_t W, int64_t pos, const double* src, int64_t n,
+                          hipStream_t stream) {
+    if (cap < 1 || W < 1 || n < 0 || pos < 0 || n > cap) return RCBF_E_BAD_SHAPE;
+    if (n == 0) return 0;
+    if (!ring || !src) return RCBF_E_NULL;
+    hipLaunchKernelGGL(k_ring_scatter, dim3((unsigned)((n * W + 255) / 256)), dim3(256), 0, stream, ring, cap, W,
+                       pos % cap, src, n);
+    return launch_status();
+}
+
+int rcbf_gather_rows_f64(double* dst, const double* ring, int64_t W, const int64_t* idx, int64_t n,
+                         hipStream_t stream) {
+    if (W < 1 || n < 0) return RCBF_E_BAD_SHAPE;
+    if (n == 0) return 0;
+    if (!dst || !ring || !idx) return RCBF_E_NULL;
+    hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((n * W + 255) / 256)), dim3(256), 0, stream, dst, ring, W, idx,
+                       n);
+    return launch_status();
+}
+
+}  // extern "C"

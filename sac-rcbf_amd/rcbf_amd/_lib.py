@@ -75,6 +75,9 @@ SIGNATURES = {
     "rcbf_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_obs_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_gp_workspace_floats": [_GPM, _I64],
+    "rcbf_model_step": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _U64, _U64, _P, _P, _P, _P, _P],
+    "rcbf_ring_scatter_f64": [_P, _I64, _I64, _I64, _P, _I64, _P],
+    "rcbf_gather_rows_f64": [_P, _P, _I64, _P, _I64, _P],
     "rcbf_gp_predict": [_GPM, _I64, _P, _P, _P, _P, _P],
     "rcbf_obs_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_cascade_u_safe": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],

@@ -56,6 +56,10 @@ def _install_stubs():
         def seed(self, s=None):
             return [s]
 
+        @property
+        def unwrapped(self):
+            return self
+
         def close(self):
             pass
 
@@ -486,6 +490,65 @@ def make_dynamics(SimulatedCarsEnv, UnicycleEnv, dynamics, seed=11):
     return out
 
 
+def make_model_rollouts(SimulatedCarsEnv, UnicycleEnv, dynamics, seed=13):
+    """rcbf_sac/generate_rollouts.py:6-81 run unmodified
+    with k_horizon=1 on fixed (obs, action, t) batches (a stub memory and agent
+    supply them) and the model prior (no GP fitted); np.random.normal is
+    routed through recorded N(0,1) draws z so the device kernel can replay
+    next = mu + std * z.  The transitions come out of the reference's own
+    ReplayMemory.batch_push (rcbf_sac/replay_memory.py:23-29)."""
+    from rcbf_sac import generate_rollouts, replay_memory
+    rng = np.random.default_rng(seed)
+    out = {}
+
+    class A:
+        gp_model_size = 2000
+        cuda = False
+
+    B = 256
+    for name, Env, n_u in (("cars", SimulatedCarsEnv, 1), ("uni", UnicycleEnv, 2)):
+        env = Env()
+        dm = dynamics.DynamicsModel(env, A())
+        if name == "cars":
+            st, _ = _rollout_cars_states(SimulatedCarsEnv, B, rng, 300)
+            obs = st.copy(); obs[:, ::2] /= 100.0; obs[:, 1::2] /= 30.0
+            t = np.round(rng.uniform(0, 6.0, B) / 0.02) * 0.02
+            t[:8] = 6.0 - 0.02  # episodes that end in this model step
+        else:
+            x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+            x[:8, :2] = np.array([2.5, 2.5]) + rng.normal(0, 0.1, (8, 2))  # near the goal
+            rel = np.array([2.5, 2.5]) - x[:, :2]
+            d = np.linalg.norm(rel, axis=1)
+            c, s_ = np.cos(x[:, 2]), np.sin(x[:, 2])
+            comp = np.stack([rel[:, 0] * c + rel[:, 1] * s_, -rel[:, 0] * s_ + rel[:, 1] * c], 1)
+            comp /= np.linalg.norm(comp, axis=1, keepdims=True) + 0.001
+            obs = np.hstack([x[:, :2], c[:, None], s_[:, None], comp, np.exp(-d)[:, None]])
+            t = np.zeros(B)
+        act = rng.uniform(-1, 1, (B, n_u))
+        z = rng.normal(0, 1, (B, obs.shape[1] if name == "cars" else 3))
+
+        class Mem:
+            def sample(self, batch_size):
+                return obs.copy(), act.copy(), np.zeros(B), obs.copy(), np.ones(B), t.copy(), t + 0.02
+
+        class Agent:
+            def select_action(self, o, dm_, warmup=False, evaluate=False):
+                return act.copy()
+
+        mm = replay_memory.ReplayMemory(10 * B, 0)
+        saved = generate_rollouts.np.random.normal
+        generate_rollouts.np.random.normal = lambda mu, sd: mu + sd * z
+        try:
+            generate_rollouts.generate_model_rollouts(env, mm, Mem(), Agent(), dm, k_horizon=1, batch_size=B)
+        finally:
+            generate_rollouts.np.random.normal = saved
+        tr = list(zip(*mm.buffer))
+        out.update({f"{name}_obs": obs, f"{name}_act": act, f"{name}_t": t, f"{name}_z": z,
+                    f"{name}_next_obs": np.stack(tr[3]), f"{name}_reward": np.asarray(tr[2], np.float64),
+                    f"{name}_mask": np.asarray(tr[4]).astype(np.float64), f"{name}_next_t": np.asarray(tr[6], np.float64)})
+    return out
+
+
 def main():
     torch.set_num_threads(8)
     SimulatedCarsEnv, UnicycleEnv, diff_cbf_qp, cbf_qp, dynamics = _import_reference()
@@ -497,6 +560,7 @@ def main():
         "env_traj.npz": lambda: make_env_traj(SimulatedCarsEnv, UnicycleEnv),
         "closed_loop_cars.npz": lambda: make_closed_loop(SimulatedCarsEnv, cbf_qp, dynamics),
         "dynamics.npz": lambda: make_dynamics(SimulatedCarsEnv, UnicycleEnv, dynamics),
+        "model_rollouts.npz": lambda: make_model_rollouts(SimulatedCarsEnv, UnicycleEnv, dynamics),
     }
     only = set(sys.argv[1:])
     for fname, fn in jobs.items():

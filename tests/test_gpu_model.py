@@ -1,0 +1,115 @@
+"""SURVEY 8f rows 3-4 on the GPU: the model-rollout step kernel against the
+reference's own generate_model_rollouts outputs (tests/golden/model_rollouts.npz,
+recorded N(0,1) draws replayed), and the device ReplayMemory against the
+reference's list semantics."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _env(mode):
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+    return BatchedSimulatedCarsEnv(4) if mode == "SimulatedCars" else BatchedUnicycleEnv(4)
+
+
+@pytest.mark.parametrize("nm,mode", [("cars", "SimulatedCars"), ("uni", "Unicycle")])
+def test_model_step_vs_reference(golden, nm, mode):
+    from rcbf_amd.generate_rollouts import model_step
+    d = golden("model_rollouts")
+    nobs, r, mask, nt = model_step(_env(mode), d[nm + "_obs"], d[nm + "_act"], d[nm + "_t"], z=d[nm + "_z"])
+    assert np.max(np.abs(nobs.cpu().numpy() - d[nm + "_next_obs"])) <= 1e-12
+    assert np.max(np.abs(r.cpu().numpy() - d[nm + "_reward"])) <= 1e-12
+    assert np.array_equal(mask.cpu().numpy(), d[nm + "_mask"])
+    assert np.array_equal(nt.cpu().numpy(), d[nm + "_next_t"])
+
+
+def test_model_step_philox_noise_and_gp_mean():
+    """In-kernel N(0,1) draws are standard normal and keyed by the counter;
+    a GP mean/std enters as mu + dt mean, std dt std (oracle)."""
+    from rcbf_amd.generate_rollouts import model_step
+    rng = np.random.default_rng(4)
+    B = 65536
+    x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+    obs = O.uni_obs(x)
+    act = rng.uniform(-1, 1, (B, 2))
+    env = _env("Unicycle")
+    n1, *_ = model_step(env, obs, act, z=None, seed=5, counter=0)
+    n2, *_ = model_step(env, obs, act, z=None, seed=5, counter=0)
+    n3, *_ = model_step(env, obs, act, z=None, seed=5, counter=1)
+    assert torch.equal(n1, n2) and not torch.equal(n1, n3)
+    base, *_ = model_step(env, obs, act, z=np.zeros((B, 3)))
+    zhat = ((n1 - base)[:, :2].cpu().numpy()) / (0.02 * 0.2)
+    assert abs(zhat.mean()) < 0.02 and abs(zhat.std() - 1.0) < 0.02
+    mean = rng.normal(0, 0.1, (B, 3)).astype(np.float32)
+    std = rng.uniform(0.01, 0.3, (B, 3)).astype(np.float32)
+    z = rng.normal(0, 1, (B, 3))
+    nobs, r, mask, nt = model_step(env, obs, act, mean=mean, std=std, z=z)
+    on, orr, om, ot = O.model_rollout_step("Unicycle", obs, act, None, z, mean=mean, std=std)
+    assert np.max(np.abs(nobs.cpu().numpy() - on)) <= 1e-12 and np.max(np.abs(r.cpu().numpy() - orr)) <= 1e-12
+
+
+def test_replay_memory_ring_and_sample():
+    from rcbf_amd.replay_memory import ReplayMemory
+    rng = np.random.default_rng(0)
+    mem = ReplayMemory(100, seed=1)
+    ref = []  # the reference's list semantics (replay_memory.py:12-21)
+    pos = 0
+    for n in (30, 50, 45, 7, 130):
+        s = rng.normal(size=(n, 10)); a = rng.normal(size=(n, 1)); r = rng.normal(size=n)
+        ns = rng.normal(size=(n, 10)); m = rng.integers(0, 2, n).astype(bool); t = rng.normal(size=n)
+        mem.batch_push(s, a, r, ns, m, t, t + 0.02)
+        for i in range(n):
+            rec = np.concatenate([s[i], a[i], [r[i]], ns[i], [float(m[i])], [t[i]], [t[i] + 0.02]])
+            if len(ref) < 100:
+                ref.append(None)
+            ref[pos] = rec
+            pos = (pos + 1) % 100
+        assert len(mem) == len(ref) and mem.position == pos
+    ring = mem._ring.cpu().numpy()
+    assert np.array_equal(ring, np.stack(ref))
+    S, A, R, NS, M, T, NT = mem.sample(64)
+    rows = np.hstack([S, A, R[:, None], NS, M[:, None], T[:, None], NT[:, None]])
+    keys = {r.tobytes() for r in np.stack(ref)}
+    assert all(r.tobytes() in keys for r in rows) and len({r.tobytes() for r in rows}) == 64  # no replacement
+    with pytest.raises(ValueError):
+        mem.sample(101)
+    mem.push(s[0], a[0], r[0], ns[0], m[0])  # single push without t
+    assert len(mem) == 100
+
+
+def test_generate_model_rollouts_end_to_end():
+    """generate_model_rollouts with device memories and a host policy:
+    every pushed transition equals the oracle step on the sampled batch."""
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.generate_rollouts import generate_model_rollouts
+    from rcbf_amd.replay_memory import ReplayMemory
+    env = _env("SimulatedCars")
+    rng = np.random.default_rng(2)
+    mem = ReplayMemory(1000, seed=3)
+    B = 500
+    st = np.tile(np.array([34.0, 30.0, 28.0, 30.0, 22.0, 30.0, 16.0, 35.0, 10.0, 30.0]), (B, 1)) + rng.normal(0, 1, (B, 10))
+    obs = st.copy(); obs[:, ::2] /= 100.0; obs[:, 1::2] /= 30.0
+    t = np.round(rng.uniform(0, 6, B) / 0.02) * 0.02
+    mem.batch_push(obs, rng.uniform(-1, 1, (B, 1)), np.zeros(B), obs, np.ones(B), t, t + 0.02)
+
+    class Agent:
+        def select_action(self, o, dm, warmup=False, evaluate=False):
+            return np.clip(o[:, 7:8] * 2 - 2, -1, 1)
+
+    mm = ReplayMemory(1000, seed=4)
+    dm = DynamicsModel(env, types.SimpleNamespace(cuda=True, gp_model_size=100))
+    generate_model_rollouts(env, mm, mem, Agent(), dm, k_horizon=1, batch_size=200)
+    assert len(mm) == 200
+    S, A, R, NS, M, T, NT = (v.cpu().numpy() for v in mm.sample_tensors(200))
+    assert np.allclose(A, np.clip(S[:, 7:8] * 2 - 2, -1, 1))
+    # replay each transition through the oracle with the kernel's own draws recovered from NS
+    base, rb, mb, tb = O.model_rollout_step("SimulatedCars", S, A, T, np.zeros((200, 10)))
+    assert np.max(np.abs(R - rb)) <= 1e-12 and np.array_equal(M, mb) and np.array_equal(NT, tb)
+    zh = (NS - base)[:, 1::2] * 30.0 / (0.02 * 0.2)
+    assert np.all(np.abs(zh) < 7) and np.array_equal(NS[:, ::2], base[:, ::2])

@@ -152,3 +152,15 @@ def test_normal_draw_distribution():
     assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
     z2 = O.normal_draw(1234, np.arange(200000), 2)
     assert abs(np.corrcoef(z, z2)[0, 1]) < 0.01
+
+
+def test_model_rollout_step_vs_reference(golden):
+    """the oracle's model-rollout step == the reference's
+    generate_model_rollouts (k_horizon = 1) on recorded N(0,1) draws."""
+    d = golden("model_rollouts")
+    for nm, mode in (("cars", "SimulatedCars"), ("uni", "Unicycle")):
+        nobs, r, mask, tn = O.model_rollout_step(mode, d[nm + "_obs"], d[nm + "_act"], d[nm + "_t"], d[nm + "_z"])
+        assert np.max(np.abs(nobs - d[nm + "_next_obs"])) <= 1e-13
+        assert np.max(np.abs(r - d[nm + "_reward"])) <= 1e-13
+        assert np.array_equal(mask, d[nm + "_mask"]) and np.array_equal(tn, d[nm + "_next_t"])
+        assert (mask == 0).sum() >= 8  # the fixture exercises episode ends / goals
