@@ -343,6 +343,77 @@ def sac_update_safe_action(env, layer, dev):
     return res
 
 
+def _time_graph(fn, reps, dev):
+    """Mean ms per fn() call, fn captured `reps` times in one hipGraph."""
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def next_rows(dev):
+    """SURVEY 8f rows 1, 3, 4 (secondary numbers, not `value`): GP posterior
+    (rcbf_gp_predict, N = gp_model_size = 3000, exact variance, cars n_s = 10)
+    as TFLOP/s of the fp32 MFMA; the model-rollout step (rcbf_model_step) and
+    the replay ring push / sample (rcbf_ring_scatter_f64 / rcbf_gather_rows_f64)
+    as rows/s and algorithmic GB/s."""
+    import ctypes
+    from rcbf_amd import _lib, gp
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv
+    from rcbf_amd.params import make_params
+    lib = _lib.load()
+    out = {}
+    rng = np.random.default_rng(0)
+    tx = rng.normal(0, 1, (3000, 10))
+    ty = 0.1 * np.sin(tx) + rng.normal(0, 0.05, (3000, 10))
+    model = gp.GPDisturbanceModel(tx, ty, [(1.5, 0.2, 0.05)] * 10, device=dev)
+    for B in (256, 4096):
+        x = torch.as_tensor(rng.normal(0, 1, (B, 10)), dtype=torch.float32, device=dev)
+        ms = _time_graph(lambda: model.predict(x), 5, dev)
+        out[f"gp_predict_N3000_B{B}"] = {"ms": round(ms, 4), "tflops": round(model.flops_per_query() * B / ms / 1e9, 1),
+                                          "frac_fp32_mfma_157TF": round(model.flops_per_query() * B / ms / 1e9 / 157.3, 3)}
+    B = 65536
+    env = BatchedSimulatedCarsEnv(4, device=dev)
+    prm = make_params(env, 1.0)
+    obs = torch.rand(B, 10, dtype=torch.float64, device=dev)
+    act = torch.rand(B, 1, dtype=torch.float64, device=dev)
+    t = torch.rand(B, dtype=torch.float64, device=dev)
+    nobs = torch.empty_like(obs)
+    r, m, nt = (torch.empty(B, dtype=torch.float64, device=dev) for _ in range(3))
+
+    def step():
+        lib.rcbf_model_step(ctypes.byref(prm), B, _lib.ptr(obs), _lib.ptr(act), _lib.ptr(t), None, None, None, 1, 0,
+                            _lib.ptr(nobs), _lib.ptr(r), _lib.ptr(m), _lib.ptr(nt), _lib.stream_of(dev))
+    ms = _time_graph(step, 20, dev)
+    out["model_step_cars_B65536"] = {"us": round(ms * 1e3, 2), "rows_per_s": round(B / ms * 1e3, 1),
+                                     "GBs": round(B * 200 / ms / 1e6, 1)}
+    W, cap = 25, 1 << 20
+    ring = torch.zeros(cap, W, dtype=torch.float64, device=dev)
+    src = torch.rand(B, W, dtype=torch.float64, device=dev)
+    ms = _time_graph(lambda: lib.rcbf_ring_scatter_f64(_lib.ptr(ring), cap, W, cap - 100, _lib.ptr(src), B,
+                                                        _lib.stream_of(dev)), 20, dev)
+    out["replay_push_B65536"] = {"us": round(ms * 1e3, 2), "GBs": round(2 * B * W * 8 / ms / 1e6, 1)}
+    for n in (256, 65536):
+        idx = torch.randint(0, cap, (n,), device=dev)
+        dst = torch.empty(n, W, dtype=torch.float64, device=dev)
+        ms = _time_graph(lambda: lib.rcbf_gather_rows_f64(_lib.ptr(dst), _lib.ptr(ring), W, _lib.ptr(idx), n,
+                                                           _lib.stream_of(dev)), 20, dev)
+        out[f"replay_sample_B{n}"] = {"us": round(ms * 1e3, 2), "GBs": round(n * (2 * W * 8 + 8) / ms / 1e6, 1)}
+    return out
+
+
 def extra_measurements(env, layer, dev, args):
     """Secondary numbers (not `value`): the K-step rollout kernel (state in
     registers across steps) and the fused step at a batch beyond the 256 MiB
@@ -361,6 +432,7 @@ def extra_measurements(env, layer, dev, args):
     ms = e0.elapsed_time(e1)
     out["rollout_K100_steps_per_s"] = round(env.num_envs * K / (ms * 1e-3), 1)
     out.update(sac_update_safe_action(env, layer, dev))
+    out.update(next_rows(dev))
     if args.env == "SimulatedCars":
         Bb = 4 * 1024 * 1024
         big = BatchedSimulatedCarsEnv(Bb, device=dev, seed=5)
