@@ -25,6 +25,17 @@ constexpr double kInf = __builtin_huge_val();
 
 // fp64 reciprocal: v_rcp_f64 + two Newton steps (error ~1 ulp), no
 // div_scale/div_fixup chain.  rcp64(0) = inf.
+// 1/d to ~11 ulp (one Newton step on v_rcp_f64, which alone is ~2^-24
+// accurate; measured, profiles/r01/ubench_fp64.txt): for the QP solvers'
+// candidate points, where a few ulps are far inside every tolerance.  The
+// bit-exact fp32 row normalisation keeps rcp64 (two steps, 0 ulp measured).
+__device__ __forceinline__ double rcp64_qp(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    return (d == 0.0) ? __builtin_copysign(__builtin_huge_val(), d) : r;
+}
+
 __device__ __forceinline__ double rcp64(double d) {
     double r = __builtin_amdgcn_rcp(d);
     double e = fma(-d, r, 1.0);
@@ -1008,15 +1019,15 @@ __device__ __forceinline__ void cars_qp_1d(const PMat<2, true>& pm, const R (*G)
     const double p0 = pm.P[0][0], p1 = pm.P[1][1];
     const double g00 = (double)G[0][0], g01 = (double)G[0][1], h0 = (double)h[0];
     const double g10 = (double)G[1][0], g11 = (double)G[1][1], h1 = (double)h[1];
-    const double U = (double)h[2] * rcp64((double)G[2][0]);
-    const double L = (double)h[3] * rcp64((double)G[3][0]);
-    const double i0 = rcp64(g01), i1 = rcp64(g11);
+    const double U = (double)h[2] * rcp64_qp((double)G[2][0]);
+    const double L = (double)h[3] * rcp64_qp((double)G[3][0]);
+    const double i0 = rcp64_qp(g01), i1 = rcp64_qp(g11);
     const double a0 = -g00 * i0, b0 = h0 * i0;  // e0(u) = a0 u + b0
     const double a1 = -g10 * i1, b1 = h1 * i1;  // e1(u) = a1 u + b1
-    const double c1 = -(p1 * a0 * b0) * rcp64(fma(p1 * a0, a0, p0));
-    const double c2 = -(p1 * a1 * b1) * rcp64(fma(p1 * a1, a1, p0));
+    const double c1 = -(p1 * a0 * b0) * rcp64_qp(fma(p1 * a0, a0, p0));
+    const double c2 = -(p1 * a1 * b1) * rcp64_qp(fma(p1 * a1, a1, p0));
     const double den = a0 - a1;
-    const double c3 = (den != 0.0) ? (b1 - b0) * rcp64(den) : 0.0;
+    const double c3 = (den != 0.0) ? (b1 - b0) * rcp64_qp(den) : 0.0;
     auto clampu = [&](double u) { return fmin(fmax(u, L), U); };
     auto phi = [&](double u) {
         double e = fmax(0.0, fmax(fma(a0, u, b0), fma(a1, u, b1)));
@@ -1066,16 +1077,16 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
     bool finite = true;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        const double inv = rcp64((double)G[j][2]);
+        const double inv = rcp64_qp((double)G[j][2]);
         a0[j] = -(double)G[j][0] * inv;
         a1[j] = -(double)G[j][1] * inv;
         b[j] = (double)h[j] * inv;
         finite = finite && isfinite(a0[j]) && isfinite(a1[j]) && isfinite(b[j]);
     }
-    const double U0 = (double)h[K] * rcp64((double)G[K][0]);
-    const double L0 = (double)h[K + 1] * rcp64((double)G[K + 1][0]);
-    const double U1 = (double)h[K + 2] * rcp64((double)G[K + 2][1]);
-    const double L1 = (double)h[K + 3] * rcp64((double)G[K + 3][1]);
+    const double U0 = (double)h[K] * rcp64_qp((double)G[K][0]);
+    const double L0 = (double)h[K + 1] * rcp64_qp((double)G[K + 1][0]);
+    const double U1 = (double)h[K + 2] * rcp64_qp((double)G[K + 2][1]);
+    const double L1 = (double)h[K + 3] * rcp64_qp((double)G[K + 3][1]);
     auto eps_of = [&](double u0, double u1) {
         double e = 0.0;
 #pragma unroll
@@ -1099,7 +1110,7 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
     for (int j = 0; j < K; ++j) {  // piece j: (diag(p0,p1) + p2 a a') u = -p2 b a
         double w0 = a0[j] * ip0, w1 = a1[j] * ip1;
         double sden = fma(p2, fma(a0[j], w0, a1[j] * w1), 1.0);
-        double f = -p2 * b[j] * rcp64(sden);
+        double f = -p2 * b[j] * rcp64_qp(sden);
         take(f * w0, f * w1);
     }
 #pragma unroll
@@ -1109,13 +1120,13 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
             double d0 = a0[i] - a0[j], d1 = a1[i] - a1[j], c = b[j] - b[i];
             double dd = fma(d0, d0, d1 * d1);
             if (dd > 1e-300) {
-                double idd = rcp64(dd);
+                double idd = rcp64_qp(dd);
                 double q0 = c * d0 * idd, q1 = c * d1 * idd;  // a point on the line
                 double n0 = -d1, n1 = d0;                     // its direction
                 double ea = fma(a0[i], q0, fma(a1[i], q1, b[i])), an = fma(a0[i], n0, a1[i] * n1);
                 double num = fma(p0 * q0, n0, fma(p1 * q1, n1, p2 * ea * an));
                 double den = fma(p0 * n0, n0, fma(p1 * n1, n1, p2 * an * an));
-                double t = -num * rcp64(den);
+                double t = -num * rcp64_qp(den);
                 take(fma(t, n0, q0), fma(t, n1, q1));
             }
         }
@@ -1130,7 +1141,7 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
                 double m10 = a0[i] - a0[l], m11 = a1[i] - a1[l], r1 = b[l] - b[i];
                 double det = fma(m00, m11, -m01 * m10);
                 if (fabs(det) > 1e-300) {
-                    double id = rcp64(det);
+                    double id = rcp64_qp(det);
                     take((r0 * m11 - r1 * m01) * id, (m00 * r1 - m10 * r0) * id);
                 }
             }
@@ -1142,7 +1153,8 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
         const double v0 = fmin(fmax(bu0, L0), U0), v1 = fmin(fmax(bu1, L1), U1);
         bf = inbox ? bf : __builtin_huge_val();  // an out-of-box stage-1 point must not win
         auto edge = [&](bool fix0, double v, double lo, double hi) {
-            // free coordinate y in [lo, hi]; e_j = al_j y + be_j
+            // free coordinate y in [lo, hi]; e_j = al_j y + be_j and
+            // phi(y) = pf y^2 + (p_fixed v^2 + p2 eps(y)^2)
             double al[K], be[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) {
@@ -1150,22 +1162,27 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
                 be[j] = fix0 ? fma(a0[j], v, b[j]) : fma(a1[j], v, b[j]);
             }
             const double pf = fix0 ? p1 : p0;
+            const double cfix = (fix0 ? p0 : p1) * v * v;
             auto cand = [&](double y) {
                 y = fmin(fmax(y, lo), hi);
-                if (fix0)
-                    take(v, y);
-                else
-                    take(y, v);
+                double e = 0.0;
+#pragma unroll
+                for (int j = 0; j < K; ++j) e = fmax(e, fma(al[j], y, be[j]));
+                const double f = fma(pf * y, y, fma(p2 * e, e, cfix));
+                const bool t = f < bf;
+                bu0 = t ? (fix0 ? v : y) : bu0;
+                bu1 = t ? (fix0 ? y : v) : bu1;
+                bf = t ? f : bf;
             };
             cand(0.0);
 #pragma unroll
-            for (int j = 0; j < K; ++j) cand(-(p2 * al[j] * be[j]) * rcp64(fma(p2 * al[j], al[j], pf)));
+            for (int j = 0; j < K; ++j) cand(-(p2 * al[j] * be[j]) * rcp64_qp(fma(p2 * al[j], al[j], pf)));
 #pragma unroll
             for (int i = 0; i < K; ++i)
 #pragma unroll
                 for (int j = i + 1; j < K; ++j) {
                     double den = al[i] - al[j];
-                    if (den != 0.0) cand((be[j] - be[i]) * rcp64(den));
+                    if (den != 0.0) cand((be[j] - be[i]) * rcp64_qp(den));
                 }
         };
         edge(true, v0, L1, U1);
@@ -1469,6 +1486,19 @@ __device__ __forceinline__ void cars_obs(const double* xs, double* o) {
     }
 }
 
+// cos/sin of (theta + d) from c = cos theta, s = sin theta, |d| <= 0.05:
+// Taylor to d^9 / d^8 (truncation < 1e-19), then the addition formulas;
+// a couple of ulps from cos/sin(theta + d) evaluated directly.
+__device__ __forceinline__ void sincos_add_small(double c, double s, double d, double& c2, double& s2) {
+    const double d2 = d * d;
+    const double sd =
+        d * fma(d2, fma(d2, fma(d2, fma(d2, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0), -1.0 / 6.0), 1.0);
+    const double cd =
+        fma(d2, fma(d2, fma(d2, fma(d2, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5), 1.0);
+    c2 = fma(c, cd, -(s * sd));
+    s2 = fma(s, cd, c * sd);
+}
+
 __device__ __forceinline__ double uni_goal_dist(const double* xs) {
 #pragma clang fp contract(off)
     double d0 = 2.5 - xs[0], d1 = 2.5 - xs[1];
@@ -1534,9 +1564,11 @@ __device__ __forceinline__ void uni_env_step(const rcbf_params& prm, double* xs,
     sincos(xs[2], &s, &c);
     xs[0] += dt * (0.0 + c * a0);
     xs[1] += dt * (0.0 + s * a0);
+    const double th0 = xs[2];
     xs[2] += dt * (0.0 + a1);
+    // cos/sin of the new theta by angle addition from the old one (|delta| <= 0.02)
     double c2, s2;
-    sincos(xs[2], &s2, &c2);
+    sincos_add_small(c, s, xs[2] - th0, c2, s2);
     const double k = dt * 0.1;
     xs[0] -= (k * c2) * c2;
     xs[1] -= (k * s2) * c2;
