@@ -164,7 +164,9 @@ typedef struct rcbf_gp_model {
     int32_t _pad;
     const float* xt;       /* (n_s, N_pad, n_s): train_x / (std + 1e-8) / (sqrt2 l_i) */
     const float* tn2;      /* (n_s, N_pad): squared norms of the xt rows             */
-    const float* Rt;       /* (n_s, N_pad, C_pad): [R_i | alpha_i | 0], R R^T = (K+nI)^-1 */
+    const float* Rt;       /* (n_s, N_pad, C_pad): [R_i | alpha_i | 0], R R^T = (K+nI)^-1;
+                              within each 128-column block, physical column 4 l + c
+                              holds logical column 32 c + l (16-B loads per lane)   */
     const double* x_std;   /* (n_s,): train_x std; queries are x / x_std (no +1e-8,
                               dynamics.py:376)                                       */
     const float* inv_sl;   /* (n_s,): 1 / (sqrt(2) l_i)                              */

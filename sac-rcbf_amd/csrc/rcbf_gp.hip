@@ -27,56 +27,64 @@ constexpr int kGpRows = 128;   // query rows per workgroup
 constexpr int kGpCols = 128;   // Rt columns per workgroup
 constexpr int kGpChunk = 256;  // training rows staged in LDS at a time
 
-// Workgroup (row tile, column block cb, GP i): 4 waves as 2 (rows) x 2 (cols),
-// each wave a 64 x 64 output = 2 x 2 tiles of 32 x 32.
+// Workgroup (row tile of 128 queries, column block cb of 128, GP i): wave w
+// owns query rows 32w..32w+31 and all 128 columns (4 tiles of 32 x 32), so
+// every A-operand value k_i(x_b, x_n) is built exactly once per workgroup and
+// each wave reduces its own rows (no cross-wave combine).  Per k-step of 2
+// training points a wave builds 1 A value per lane (10 fma + exp2) and
+// issues 4 MFMAs; the B values of the next 4 k-steps are loaded while the
+// current ones are consumed (register double buffer).
 // partial[(i * n_cb + cb) * B + b] = sum over this block's columns j < r of Q^2;
 // meanraw[i * B + b] = Q(b, r) from the block holding column r.
-template <int D>
+template <int D, int CT>
 __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
                                                   float* __restrict__ partial, float* __restrict__ meanraw) {
     constexpr int DP = (D + 3) / 4 * 4;  // LDS row stride (float4 reads)
+    constexpr float kL2E = 1.4426950408889634f;
     __shared__ float4 s_xt[kGpChunk * DP / 4];
-    __shared__ float s_tn2[kGpChunk];
-    __shared__ float s_rows[kGpRows];
+    __shared__ float s_tn[kGpChunk];
 
+    // CT column tiles of 32 per wave: 4 (the whole 128-column block) or 2
+    // (half of it, twice the workgroups for small query batches)
     const int i = blockIdx.z;
-    const int cb = blockIdx.y;
-    const int n_cb = gridDim.y;
+    const int cb = blockIdx.y / (4 / CT);          // 128-column block
+    const int sub = blockIdx.y % (4 / CT);         // which CT tiles of it
+    const int n_part = gridDim.y;
     const int64_t b0 = (int64_t)blockIdx.x * kGpRows;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int rw = (w >> 1) * 64, cw = (w & 1) * 64;
     const int half = lane >> 5, l32 = lane & 31;
     const float sl = m.inv_sl[i];
-    const float s_i = m.outscale[i];
+    const float log2s = __log2f(m.outscale[i]);
 
-    // this lane's two query rows (A operand row = lane & 31 of each row tile)
-    float xs[2][D], qn2[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        int64_t row = b0 + rw + t * 32 + l32;
+    // A(b, n) = s exp(-|xs_b - xt_n|^2) = exp2(log2 s - L2E |xs|^2 - L2E |xt|^2 + 2 L2E xs.xt)
+    float xs2[D], q0;
+    {
+        int64_t row = b0 + 32 * w + l32;
         row = row < B ? row : B - 1;
-        float acc = 0.0f;
+        float nrm = 0.0f;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             // dynamics.py:376: test_x / train_x_std in fp64, then .float()
-            float xn = (float)((double)xq[row * D + k] / m.x_std[k]);
-            xs[t][k] = xn * sl;
-            acc = fmaf(xs[t][k], xs[t][k], acc);
+            const float xs = (float)((double)xq[row * D + k] / m.x_std[k]) * sl;
+            nrm = fmaf(xs, xs, nrm);
+            xs2[k] = 2.0f * kL2E * xs;
         }
-        qn2[t] = acc;
+        q0 = fmaf(-kL2E, nrm, log2s);
     }
 
-    f32x16 acc[2][2];
+    f32x16 acc[CT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int c = 0; c < CT; ++c)
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[t][c][r] = 0.0f;
+        for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
 
     const float* xt_i = m.xt + (int64_t)i * m.N_pad * D;
     const float* tn2_i = m.tn2 + (int64_t)i * m.N_pad;
-    const float* Rt_i = m.Rt + (int64_t)i * m.N_pad * m.C_pad + (int64_t)cb * kGpCols + cw + l32;
+    const int64_t ldc = m.C_pad;
+    // Rt columns are stored lane-interleaved per 128-column block (physical
+    // 4 l + c holds logical column 32 c + l), so one dwordx4 load gives a lane
+    // its B values for the 4 column tiles.
+    const float* Rt_i = m.Rt + (int64_t)i * m.N_pad * ldc + (int64_t)cb * kGpCols + 4 * l32 + CT * sub;
 
     for (int n0 = 0; n0 < m.N_pad; n0 += kGpChunk) {
         const int nch = min(kGpChunk, m.N_pad - n0);  // multiple of 32
@@ -86,87 +94,73 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
 #pragma unroll
             for (int k = 0; k < DP; ++k) v[k] = k < D ? xt_i[(int64_t)(n0 + e) * D + k] : 0.0f;
 #pragma unroll
-            for (int q = 0; q < DP / 4; ++q) s_xt[e * (DP / 4) + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-            s_tn2[e] = tn2_i[n0 + e];
+            for (int q = 0; q < DP / 4; ++q)
+                s_xt[e * (DP / 4) + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+            s_tn[e] = -kL2E * tn2_i[n0 + e];
         }
         __syncthreads();
-        // B operand: Rt[n][col], n = k-step row of this half-wave
-        const float* rp = Rt_i + (int64_t)(n0 + half) * m.C_pad;
-        for (int k8 = 0; k8 < nch; k8 += 8)
+        // B operand of k-step kk: Rt[n0 + kk + half][cb*128 + 32c + l32]
+        const float* rp = Rt_i + (int64_t)(n0 + half) * ldc;
+        float bcur[4][CT], bnx[4][CT];
+        auto ldb = [&](int k, float* dst) {
+            if constexpr (CT == 4) {
+                const float4 v = *reinterpret_cast<const float4*>(rp + (int64_t)k * ldc);
+                dst[0] = v.x, dst[1] = v.y, dst[2] = v.z, dst[3] = v.w;
+            } else {
+                const float2 v = *reinterpret_cast<const float2*>(rp + (int64_t)k * ldc);
+                dst[0] = v.x, dst[1] = v.y;
+            }
+        };
 #pragma unroll
-        for (int kq = 0; kq < 8; kq += 2) {
-            const int kk = k8 + kq;
-            const int nl = kk + half;
-            float bv0 = rp[(int64_t)kk * m.C_pad];
-            float bv1 = rp[(int64_t)kk * m.C_pad + 32];
-            float4 xt4[DP / 4];
+        for (int q = 0; q < 4; ++q) ldb(2 * q, bcur[q]);
+        for (int k8 = 0; k8 < nch; k8 += 8) {
+            const bool more = k8 + 8 < nch;
 #pragma unroll
-            for (int q = 0; q < DP / 4; ++q) xt4[q] = s_xt[nl * (DP / 4) + q];
-            const float* xtv = reinterpret_cast<const float*>(xt4);
-            const float tn = s_tn2[nl];
-            float av[2];
+            for (int q = 0; q < 4; ++q) {
+                if (more)
+                    ldb(k8 + 8 + 2 * q, bnx[q]);
+                else
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                float dot = 0.0f;
-#pragma unroll
-                for (int k = 0; k < D; ++k) dot = fmaf(xs[t][k], xtv[k], dot);
-                float d2 = fmaxf(qn2[t] + tn - 2.0f * dot, 0.0f);
-                av[t] = s_i * __expf(-d2);
+                    for (int c = 0; c < CT; ++c) bnx[q][c] = 0.0f;
             }
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                acc[t][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], bv0, acc[t][0], 0, 0, 0);
-                acc[t][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[t], bv1, acc[t][1], 0, 0, 0);
+            for (int q = 0; q < 4; ++q) {
+                const int nl = k8 + 2 * q + half;
+                float4 xt4[DP / 4];
+#pragma unroll
+                for (int u = 0; u < DP / 4; ++u) xt4[u] = s_xt[nl * (DP / 4) + u];
+                const float* xtv = reinterpret_cast<const float*>(xt4);
+                float arg = q0 + s_tn[nl];
+#pragma unroll
+                for (int k = 0; k < D; ++k) arg = fmaf(xs2[k], xtv[k], arg);
+                const float av = __builtin_amdgcn_exp2f(fminf(arg, log2s));
+#pragma unroll
+                for (int c = 0; c < CT; ++c)
+                    acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bcur[q][c], acc[c], 0, 0, 0);
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int c = 0; c < CT; ++c) bcur[q][c] = bnx[q][c];
         }
     }
 
     // epilogue: C layout col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
     const int r_rank = m.r;
-    float rs[2][16];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int r = 0; r < 16; ++r) {
+        const int64_t row = b0 + 32 * w + (r & 3) + 8 * (r >> 2) + 4 * half;
+        float v = 0.0f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            float v = 0.0f;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int col = cb * kGpCols + cw + c * 32 + l32;
-                const float q = acc[t][c][r];
-                v += (col < r_rank) ? q * q : 0.0f;
-                if (col == r_rank) {
-                    const int64_t row = b0 + rw + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                    if (row < B) meanraw[(int64_t)i * B + row] = q;
-                }
-            }
-            rs[t][r] = v;
+        for (int c = 0; c < CT; ++c) {
+            const int col = cb * kGpCols + 32 * (c + CT * sub) + l32;
+            const float q = acc[c][r];
+            v += (col < r_rank) ? q * q : 0.0f;
+            if (col == r_rank && row < B) meanraw[(int64_t)i * B + row] = q;
         }
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            float v = rs[t][r];
-#pragma unroll
-            for (int msk = 1; msk < 32; msk <<= 1) v += __shfl_xor(v, msk, 64);
-            rs[t][r] = v;
-        }
-    // combine the two column-waves of each row half in a fixed order
-    if ((w & 1) == 0 && l32 == 0) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s_rows[rw + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * half] = rs[t][r];
-    }
-    __syncthreads();
-    if ((w & 1) == 1 && l32 == 0) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int lr = rw + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                const int64_t row = b0 + lr;
-                if (row < B) partial[((int64_t)i * n_cb + cb) * B + row] = s_rows[lr] + rs[t][r];
-            }
+        for (int msk = 1; msk < 32; msk <<= 1) v += __shfl_xor(v, msk, 64);
+        if (l32 == 0 && row < B) partial[((int64_t)i * n_part + blockIdx.y) * B + row] = v;
     }
 }
 
@@ -194,7 +188,7 @@ extern "C" {
 int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B) {
     if (!m || B < 0) return -1;
     const int64_t n_cb = m->C_pad / kGpCols;
-    return (int64_t)m->n_s * (n_cb + 1) * B;
+    return (int64_t)m->n_s * (2 * n_cb + 1) * B;  // partials for up to 2 launches per block, + means
 }
 
 int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out, float* std_out,
@@ -208,22 +202,27 @@ int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* me
         !m->outscale || !m->noise || !m->y_scale)
         return RCBF_E_NULL;
     const int n_cb = m->C_pad / kGpCols;
+    // CT = 2 (half-width column tiles, twice the workgroups) measured no faster
+    // at B = 256 (profiles/r01/gp_predict_roofline.jsonl), so every batch uses CT = 4
+    const int n_part = n_cb;
     float* partial = workspace;
-    float* meanraw = workspace + (int64_t)m->n_s * n_cb * B;
-    dim3 g((unsigned)((B + kGpRows - 1) / kGpRows), (unsigned)n_cb, (unsigned)m->n_s);
+    float* meanraw = workspace + (int64_t)m->n_s * 2 * n_cb * B;
+    dim3 g((unsigned)((B + kGpRows - 1) / kGpRows), (unsigned)n_part, (unsigned)m->n_s);
+#define RCBF_GP_L(DD) hipLaunchKernelGGL((k_gp_qform<DD, 4>), g, dim3(256), 0, stream, *m, B, x, partial, meanraw)
     switch (m->n_s) {  // D = n_s: the GP inputs are the full state
         case 3:
-            hipLaunchKernelGGL((k_gp_qform<3>), g, dim3(256), 0, stream, *m, B, x, partial, meanraw);
+            RCBF_GP_L(3);
             break;
         case 10:
-            hipLaunchKernelGGL((k_gp_qform<10>), g, dim3(256), 0, stream, *m, B, x, partial, meanraw);
+            RCBF_GP_L(10);
             break;
         default:
             return RCBF_E_BAD_SHAPE;
     }
+#undef RCBF_GP_L
     const int64_t tot = B * m->n_s;
-    hipLaunchKernelGGL(k_gp_finish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *m, B, n_cb, partial,
-                       meanraw, mean_out, std_out);
+    hipLaunchKernelGGL(k_gp_finish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *m, B, n_part,
+                       partial, meanraw, mean_out, std_out);
     return launch_status();
 }
 

@@ -112,7 +112,9 @@ class GPDisturbanceModel:
             Rt[i, :N, self.r] = alpha.float()
         self.xt = xt.contiguous()
         self.tn2 = (xt.double() ** 2).sum(-1).float().contiguous()
-        self.Rt = Rt.contiguous()
+        # lane-interleave each 128-column block: physical 4 l + c <- logical 32 c + l
+        n_cb = C_pad // _PAD_C
+        self.Rt = Rt.view(n_s, N_pad, n_cb, 4, 32).permute(0, 1, 2, 4, 3).contiguous().view(n_s, N_pad, C_pad)
         self.x_std = torch.as_tensor(x_std, dtype=torch.float64, device=dev)
         self.inv_sl = torch.tensor([1.0 / (math.sqrt(2.0) * h[0]) for h in self.hyper], dtype=torch.float32, device=dev)
         self.outscale = torch.tensor([h[1] for h in self.hyper], dtype=torch.float32, device=dev)
@@ -121,6 +123,11 @@ class GPDisturbanceModel:
         self._m = _lib.RcbfGpModel(n_s, N, N_pad, self.r, C_pad, 0, *(t.data_ptr() for t in (
             self.xt, self.tn2, self.Rt, self.x_std, self.inv_sl, self.outscale, self.noise, self.y_scale)))
         self._ws = torch.empty(0, dtype=torch.float32, device=dev)
+
+    def logical_Rt(self):
+        """(n_s, N_pad, C_pad) [R | alpha | 0] in logical column order."""
+        n_s, N_pad, C_pad = self.Rt.shape
+        return self.Rt.view(n_s, N_pad, C_pad // _PAD_C, 32, 4).permute(0, 1, 2, 4, 3).reshape(n_s, N_pad, C_pad)
 
     def predict(self, x):
         """x (B, n_s) float32 device tensor -> (mean, std) (B, n_s) float32."""

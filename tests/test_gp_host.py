@@ -47,7 +47,7 @@ def test_device_layout_reproduces_exact_posterior(n_s, N, rank):
     xq = (q / tx.std(0)).astype(np.float32).astype(np.float64)
     mean = np.zeros_like(xq)
     std = np.zeros_like(xq)
-    Rt = m.Rt.double().numpy()
+    Rt = m.logical_Rt().double().numpy()
     for i in range(n_s):
         xs = xq * float(m.inv_sl[i])
         xt = m.xt[i].double().numpy()
