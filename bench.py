@@ -141,9 +141,8 @@ def init_states(env, gen, env_name):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from rcbf_amd import shard
+    rank, local, world = shard.world_info()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -159,10 +158,10 @@ def main():
     B = args.batch
     solver = _lib.SOLVER_PDIPM if args.solver == "pdipm" else _lib.SOLVER_ACTIVE_SET
     if args.env == "SimulatedCars":
-        env = BatchedSimulatedCarsEnv(B, device=dev, seed=1234, env_offset=rank * B)
+        env = BatchedSimulatedCarsEnv(B, device=dev, seed=1234, env_offset=shard.env_offset(rank, B))
     else:
         from oracle.oracle import UNI  # constants only
-        env = BatchedUnicycleEnv(B, device=dev, seed=1234, env_offset=rank * B,
+        env = BatchedUnicycleEnv(B, device=dev, seed=1234, env_offset=shard.env_offset(rank, B),
                                  hazards_locations=UNI["hazards"][:args.hazards])
     layer = CBFQPLayer(env, LArgs(), gamma_b=20.0, solver=solver)
     S = largest_divisor_le(args.steps, args.graph_steps)
@@ -205,8 +204,7 @@ def main():
 
     reps = args.steps // S
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
+    shard.barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()
@@ -214,21 +212,13 @@ def main():
         graph.replay()
     ev1.record()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    shard.barrier(world)
     el = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # per fused-step launch, on the launch stream
     env.check_failures()
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        k = torch.tensor([kern_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(k, op=dist.ReduceOp.MAX)
-        kern_ms = float(k.item())
-
-    total_steps = world * B * args.steps
-    value = total_steps / el
+    el = shard.max_over_ranks(el, world, dev)
+    kern_ms = shard.max_over_ranks(kern_ms, world, dev)
+    value = shard.whole_job_rate(world, B, args.steps, el)
     bps = BYTES_PER_STEP[args.env]
     achieved = B * bps / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.env, B)

@@ -1,0 +1,86 @@
+"""The N > 1 path on CPU (gloo, world_size 2): the shard layout, barrier and
+max-over-ranks reduction bench.py uses (rcbf_amd.shard), and sharding
+invariance of the batched episode stream -- each rank steps its contiguous
+shard with auto-resets whose N(0, 0.5) draw is keyed by the GLOBAL env index
+(the device RNG restated by the oracle), and the gathered result equals the
+unsharded run bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+
+B_TOTAL, STEPS, SEED = 64, 310, 9
+
+
+def _run_shard(x, t, st, ep, offset, u_seq):
+    """Oracle cars episodes with auto-reset for envs [offset, offset + len(x))."""
+    x, t, st, ep = x.copy(), t.copy(), st.copy(), ep.copy()
+    for k in range(STEPS):
+        u = u_seq[k, offset:offset + x.shape[0]]
+        x, t, st, obs, r, c, done = O.cars_step(x, t, st, u)
+        if done.any():
+            idx = np.nonzero(done)[0]
+            ep[idx] += 1
+            nz = 0.5 * O.normal_draw(SEED, offset + idx, ep[idx])
+            xr, tr, sr = O.cars_reset(nz)
+            x[idx], t[idx], st[idx] = xr, tr, sr
+    return x, ep
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from rcbf_amd import shard
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r, lr, w = shard.world_info()
+    per = B_TOTAL // w
+    off = shard.env_offset(r, per)
+    rng = np.random.default_rng(0)
+    u_seq = rng.uniform(-1, 1, (STEPS, B_TOTAL, 1)).astype(np.float32)
+    ep = np.ones(per, np.int64)
+    x0, t0, st0 = O.cars_reset(0.5 * O.normal_draw(SEED, off + np.arange(per), ep))
+    shard.barrier(w)
+    xs, eps = _run_shard(x0, t0, st0, ep, off, u_seq)
+    shard.barrier(w)
+    el = shard.max_over_ranks(0.5 + r, w, "cpu")  # rank 1 is "slower"
+    gx = [torch.zeros(per, 10, dtype=torch.float64) for _ in range(w)]
+    dist.all_gather(gx, torch.as_tensor(xs))
+    if r == 0:
+        q.put((torch.cat(gx).numpy(), el, shard.whole_job_rate(w, per, STEPS, el)))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_gloo_shards_reproduce_unsharded_run():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    x_sharded, el, rate = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # unsharded reference run
+    rng = np.random.default_rng(0)
+    u_seq = rng.uniform(-1, 1, (STEPS, B_TOTAL, 1)).astype(np.float32)
+    ep = np.ones(B_TOTAL, np.int64)
+    x0, t0, st0 = O.cars_reset(0.5 * O.normal_draw(SEED, np.arange(B_TOTAL), ep))
+    x_full, _ = _run_shard(x0, t0, st0, ep, 0, u_seq)
+    assert np.array_equal(x_sharded, x_full)
+    assert el == 1.5  # max over ranks
+    assert rate == pytest.approx(2 * (B_TOTAL // 2) * STEPS / 1.5)
