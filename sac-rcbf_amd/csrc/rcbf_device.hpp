@@ -1449,10 +1449,13 @@ __device__ __forceinline__ void cars_env_step(const rcbf_params& prm, double* xs
     double v[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) v[i] = xs[2 * i + 1];
+    // x += dt * (f + g u): the reference adds g u = 0.0 to every component but
+    // car 3's velocity; v + 0.0 differs from v only for v = -0.0, and then only
+    // in the sign of a zero, so those adds are skipped.
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-        xs[2 * i] += dt * (v[i] + 0.0);
-        xs[2 * i + 1] += dt * (acc[i] + (i == 3 ? gu : 0.0));
+        xs[2 * i] += dt * v[i];
+        xs[2 * i + 1] += dt * (i == 3 ? acc[i] + gu : acc[i]);
     }
     t = t + dt;
     step += 1;
@@ -1562,10 +1565,11 @@ __device__ __forceinline__ void uni_env_step(const rcbf_params& prm, double* xs,
     const double dt = 0.02;
     double c, s;
     sincos(xs[2], &s, &c);
-    xs[0] += dt * (0.0 + c * a0);
-    xs[1] += dt * (0.0 + s * a0);
+    // f = 0: 0.0 + g u equals g u up to the sign of a zero (skipped)
+    xs[0] += dt * (c * a0);
+    xs[1] += dt * (s * a0);
     const double th0 = xs[2];
-    xs[2] += dt * (0.0 + a1);
+    xs[2] += dt * a1;
     // cos/sin of the new theta by angle addition from the old one (|delta| <= 0.02)
     double c2, s2;
     sincos_add_small(c, s, xs[2] - th0, c2, s2);
