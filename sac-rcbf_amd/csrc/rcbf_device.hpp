@@ -1044,9 +1044,12 @@ __device__ __forceinline__ void cars_qp_1d(const PMat<2, true>& pm, const R (*G)
     ub = (f3 < fb) ? u3 : ub;
     z[0] = ub;
     z[1] = fmax(0.0, fmax(fma(a0, ub, b0), fma(a1, ub, b1)));
-    bool ok = isfinite(z[0]) && isfinite(z[1]) && (L <= U);
-    status = ok ? RCBF_QP_OK : (isfinite(g00 + g01 + h0 + g10 + g11 + h1 + U + L) ? RCBF_QP_INFEASIBLE
-                                                                               : RCBF_QP_NONFINITE);
+    // fmin/fmax drop NaNs, so non-finite data must be caught on the inputs:
+    // the reference's solver returns NaN there and the layer raises (diff_cbf_qp.py:141-143)
+    const bool fin = isfinite(g00 + g01 + h0 + g10 + g11 + h1 + U + L + a0 + a1 + b0 + b1);
+    const bool ok = fin && isfinite(z[0]) && isfinite(z[1]) && (L <= U);
+    status = ok ? RCBF_QP_OK : (fin ? RCBF_QP_INFEASIBLE : RCBF_QP_NONFINITE);
+    if (!fin) z[0] = z[1] = __builtin_nan("");
 }
 
 // Exact solver for the UNICYCLE QP structure (both formulations), z = (u0, u1, eps):
@@ -1191,8 +1194,10 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
     z[0] = bu0;
     z[1] = bu1;
     z[2] = eps_of(bu0, bu1);
+    finite = finite && isfinite(U0 + L0 + U1 + L1);  // fmin/fmax would hide a NaN bound
     const bool ok = isfinite(z[0]) && isfinite(z[1]) && isfinite(z[2]) && bf < __builtin_huge_val();
     status = !finite ? RCBF_QP_NONFINITE : (ok && L0 <= U0 && L1 <= U1 ? RCBF_QP_OK : RCBF_QP_INFEASIBLE);
+    if (!finite) z[0] = z[1] = z[2] = __builtin_nan("");
 }
 
 // Compile-time solver choice (the host dispatches on rcbf_params.solver):

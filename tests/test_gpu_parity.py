@@ -414,3 +414,51 @@ def test_large_batch_properties():
     stat = Pd * z + np.einsum("bmn,bm->bn", Gn.astype(np.float64), lm)
     assert np.abs(stat).max() <= 1e-4 * (1 + np.abs(lm).max())  # stationarity
     assert np.abs(lm * viol).max() <= 1e-4                      # complementarity
+
+
+# ----------------------------------------------------------------------------
+# failure paths (diff_cbf_qp.py:141-143, cbf_qp.py:279-281)
+# ----------------------------------------------------------------------------
+@pytest.mark.parametrize("solver", [0, 1, 2])
+def test_nan_input_raises_qp_failed(golden, solver):
+    d = golden("cars_layer")
+    layer = _layer(_env("SimulatedCars"), float(d["gamma_b"]), solver)
+    x, u, mu, sg = (dev(d["prior" + k][:64]) for k in ("_x", "_u", "_mu", "_sigma"))
+    x[5, 4] = float("nan")
+    with pytest.raises(Exception, match="QP Failed to solve"):
+        layer.get_safe_action(x, u, mu, sg)
+    P, q, G, h = layer.get_cbf_qp_constraints(x, u, mu, sg)
+    with pytest.raises(Exception, match="QP Failed to solve"):
+        layer.solve_qp(P, q, G, h)
+    x[5, 4] = 1.0  # a clean batch solves again on the same layer
+    assert torch.isfinite(layer.get_safe_action(x, u, mu, sg)).all()
+
+
+def test_fused_step_failure_flag_and_status():
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv
+    B = 256
+    x, t, st = _cars_states(B, 31)
+    x[17, 6] = np.nan
+    env = BatchedSimulatedCarsEnv(B)
+    env.load_state(x, t, st)
+    layer = _layer(env, 20.0)
+    outs = env.make_outputs()
+    env.safe_step(dev(np.zeros((B, 1))), layer, auto_reset=False, outputs=outs)
+    with pytest.raises(Exception, match="QP Failed to solve"):
+        env.check_failures()
+    env.check_failures()  # the flag was cleared by the raise
+    u = outs["u"].cpu().numpy()
+    assert np.isfinite(np.delete(u, 17, axis=0)).all()
+
+
+def test_cascade_nan_raises_value_error():
+    from rcbf_amd.cbf_qp import CascadeCBFLayer
+    env = _env("SimulatedCars")
+    layer = CascadeCBFLayer(env, gamma_b=20.0, k_d=3.0)
+    s = np.array([34.0, 30.0, 28.0, 30.0, 22.0, 30.0, 16.0, 35.0, 10.0, 30.0])
+    assert np.all(np.isfinite(layer.get_u_safe(np.array([0.5]), s, np.zeros(10), np.zeros(10))))
+    s[3] = np.nan  # car 1's velocity does not enter the cars CBF rows (cbf_qp.py:155-240): no failure
+    assert np.all(np.isfinite(layer.get_u_safe(np.array([0.5]), s, np.zeros(10), np.zeros(10))))
+    s[6] = np.nan  # car 3's position does
+    with pytest.raises(ValueError):
+        layer.get_u_safe(np.array([0.5]), s, np.zeros(10), np.zeros(10))
