@@ -43,7 +43,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--batch", type=int, default=65536,
+                    help="envs per GPU (weak scaling) or in total (--scaling strong)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --batch envs on every GPU; strong: --batch envs split over the GPUs")
     ap.add_argument("--env", default="SimulatedCars", choices=["SimulatedCars", "Unicycle"])
     ap.add_argument("--hazards", type=int, default=3, help="unicycle hazard count")
     ap.add_argument("--solver", default="active_set", choices=["active_set", "pdipm"])
@@ -143,6 +146,10 @@ def main():
     args = parse()
     from rcbf_amd import shard
     rank, local, world = shard.world_info()
+    if args.scaling == "strong":
+        if args.batch % world:
+            raise SystemExit("--scaling strong needs --batch divisible by the GPU count")
+        args.batch //= world
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -234,7 +241,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(el / args.steps * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32 rows / f64 QP / f64 env",
         "data": "synthetic (SURVEY 8(d) start states, u_RL ~ U[-1,1], prior mean/sigma, seeded auto-resets)",

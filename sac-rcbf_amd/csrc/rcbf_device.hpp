@@ -234,6 +234,7 @@ struct QPResult {
     int nact;
     int status;        // RCBF_QP_*
     int iters;
+    bool certified;    // PDIPM: the polished point passed the KKT check
 };
 
 // Active rows are tracked in N slots (|A| <= n for a strictly convex QP with
@@ -754,6 +755,7 @@ __device__ __forceinline__ void pdipm_solve(const PMat<N, DIAG>& pm, const doubl
     double z[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) z[k] = bx[k];
+    out.certified = false;
     if (finite) {
         double x0[N];
         pm.inv_apply(q, x0);
@@ -769,6 +771,8 @@ __device__ __forceinline__ void pdipm_solve(const PMat<N, DIAG>& pm, const doubl
         for (int sl = 0; sl < N; ++sl) ok = ok && (sl >= A.n || A.lam[sl] >= -1e-9);
 #pragma unroll
         for (int k = 0; k < N; ++k) z[k] = ok ? zp[k] : z[k];
+        out.certified = ok;
+        if (ok) status = RCBF_QP_OK;  // a certified KKT point is the optimum, however many iterations it took
     }
     bool okf = true;
 #pragma unroll
@@ -1210,6 +1214,14 @@ __device__ __forceinline__ void qp_solve(const PMat<N, DIAG>& pm, const double* 
                                          const R* h, int max_iter, double eps, QPResult<N, M>& out) {
     if constexpr (SOLVER == RCBF_SOLVER_PDIPM) {
         pdipm_solve<N, M, DIAG, R>(pm, q, G, h, max_iter > 0 ? max_iter : 50, eps > 0 ? eps : 1e-10, out);
+        // qpth returns its best iterate when it stalls (notImprovedLim), which
+        // can be far from the optimum on badly scaled rows; a point that fails
+        // the KKT certificate is re-solved exactly instead (rare lanes only).
+        if (!out.certified && out.status != RCBF_QP_NONFINITE) {
+            const int its = out.iters;
+            gi_solve<N, M, DIAG, R>(pm, q, G, h, 4 * (M + N) + 8, out);
+            out.iters = its;
+        }
     } else if constexpr (SOLVER == RCBF_SOLVER_ACTIVE_SET && N == 2 && DIAG) {
 #if defined(RCBF_ENUM2_FP64_ONLY)
         enum2_solve<M, R>(pm, G, h, out);

@@ -1,0 +1,6 @@
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=gpurun_out/$1; mkdir -p $OUT
+timeout -k 10 200 python bench.py --no-cpu-baseline --solver pdipm > $OUT/pdipm_cars.log 2>&1 || exit 1
+timeout -k 10 200 python bench.py --no-cpu-baseline --solver pdipm --env Unicycle > $OUT/pdipm_uni.log 2>&1 || exit 1
+timeout -k 10 200 python bench.py --no-cpu-baseline --scaling strong > $OUT/strong1.log 2>&1 || exit 1

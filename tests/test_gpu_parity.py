@@ -462,3 +462,28 @@ def test_cascade_nan_raises_value_error():
     s[6] = np.nan  # car 3's position does
     with pytest.raises(ValueError):
         layer.get_u_safe(np.array([0.5]), s, np.zeros(10), np.zeros(10))
+
+
+@pytest.mark.parametrize("mode", ["SimulatedCars", "Unicycle"])
+def test_pdipm_agrees_with_exact_solver_at_scale(mode):
+    """The qpth-style IPM (solver 1) returns the exact optimum on 65536
+    SURVEY 8(d) states: stalled iterates (qpth's notImprovedLim exit) that fail
+    the KKT certificate are re-solved exactly (found at x = (-1.45, -1.35,
+    3.0): the stalled iterate was 3.0 off)."""
+    rng = np.random.default_rng(0)
+    B = 65536
+    if mode == "Unicycle":
+        hz = O.UNI["hazards"][:3]
+        env = _env(mode, hz)
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        s32 = O.get_state_f32(mode, O.uni_obs(x).astype(np.float32))
+    else:
+        env = _env(mode)
+        xs, _, _ = _cars_states(B, 40)
+        s32 = O.get_state_f32(mode, O.cars_obs(xs).astype(np.float32))
+    mu, sg = O.predict_disturbance_prior(mode, B)
+    u = rng.uniform(-1, 1, (B, env.n_u)).astype(np.float32)
+    args = [dev(v) for v in (s32, u, mu.astype(np.float32), sg.astype(np.float32))]
+    a = _layer(env, 20.0, 0).get_safe_action(*args)
+    b = _layer(env, 20.0, 1).get_safe_action(*args)
+    assert float((a - b).abs().max()) <= 1e-5
