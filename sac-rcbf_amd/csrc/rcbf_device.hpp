@@ -1445,10 +1445,15 @@ struct CarsStepOut {
 };
 
 // SimulatedCarsEnv.step (simulated_cars_env.py:38-106): true dynamics with
-// the lead car's sin term, car 4's kp drift kept, x1.1 on every acceleration.
-template <typename A>
-__device__ __forceinline__ void cars_env_step(const rcbf_params& prm, double* xs, double& t, int& step, A action,
-                                              CarsStepOut& o) {
+// the lead car's sin term, car 4's kp drift kept, x1.1 on every acceleration,
+// split at the safe action: cars_env_pre is everything
+// that does not depend on it (all positions, the velocities of cars 0, 1, 2
+// and 4, t, step, done, cost) and returns car 3's acceleration; cars_env_post
+// adds g u to car 3's velocity and forms the reward.  pre + post is exactly
+// the reference's step.  (Storing the pre part before the QP so its writes
+// overlap the QP measured no faster: profiles/r01/ablate_early_store.txt.)
+__device__ __forceinline__ double cars_env_pre(const rcbf_params& prm, double* xs, double& t, int& step,
+                                               CarsStepOut& o) {
 #pragma clang fp contract(off)
     const double kp = prm.kp, kb = prm.k_brake, dt = 0.02;
     double vdes0 = 30.0 - 10.0 * sin_small(0.2 * t);
@@ -1462,7 +1467,6 @@ __device__ __forceinline__ void cars_env_step(const rcbf_params& prm, double* xs
     acc[4] += (-kb * d24) * (d24 < 13.0 ? 1.0 : 0.0);
 #pragma unroll
     for (int i = 0; i < 5; ++i) acc[i] *= 1.1;
-    const double gu = 50.0 * (double)action;
     double v[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) v[i] = xs[2 * i + 1];
@@ -1472,20 +1476,37 @@ __device__ __forceinline__ void cars_env_step(const rcbf_params& prm, double* xs
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
         xs[2 * i] += dt * v[i];
-        xs[2 * i + 1] += dt * (i == 3 ? acc[i] + gu : acc[i]);
+        if (i != 3) xs[2 * i + 1] += dt * acc[i];
     }
     t = t + dt;
     step += 1;
     o.done = step >= 300;
+    double cost = 0.0;
+    if (xs[4] - xs[6] < 2.99) cost -= 0.1;
+    if (xs[6] - xs[8] < 2.99) cost -= 0.1;
+    o.cost = cost;
+    return acc[3];
+}
+
+template <typename A>
+__device__ __forceinline__ void cars_env_post(double* xs, double acc3, A action, CarsStepOut& o) {
+#pragma clang fp contract(off)
+    const double dt = 0.02;
+    const double gu = 50.0 * (double)action;
+    xs[7] += dt * (acc3 + gu);
     // reward in the action's dtype (-5.0 * abs(a**2) / 300), :93
     A a2 = action * action;
     A r = (A)(-5.0) * (a2 < (A)0 ? -a2 : a2) / (A)300;
     o.reward = (float)r;
     o.reward_d = (double)r;
-    double cost = 0.0;
-    if (xs[4] - xs[6] < 2.99) cost -= 0.1;
-    if (xs[6] - xs[8] < 2.99) cost -= 0.1;
-    o.cost = cost;
+}
+
+// SimulatedCarsEnv.step (simulated_cars_env.py:38-106)
+template <typename A>
+__device__ __forceinline__ void cars_env_step(const rcbf_params& prm, double* xs, double& t, int& step, A action,
+                                              CarsStepOut& o) {
+    const double acc3 = cars_env_pre(prm, xs, t, step, o);
+    cars_env_post<A>(xs, acc3, action, o);
 }
 
 // x / d for a constant d, correctly rounded: q = RN(x * RN(1/d)) is within
