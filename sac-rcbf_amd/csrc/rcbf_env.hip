@@ -213,14 +213,6 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B
     bool dn, gm;
     int status;
     RCBF_STAMP(stamps, 1, true);
-        st_out(&u_out[i], uf[0]);
-        st_out(&reward[i], o.reward);
-        RCBF_STAMP(stamps, 6, false);
-        report(status, status_out, i, fail_flag);
-        RCBF_STAMP(stamps, 7, true);
-        return;
-    }
-#endif
     double oc[4] = {0.0, 0.0, 0.0, 0.0};
     safe_step_one<SOLVER, MODE, K>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
                                    seed, off, stamps, oc, RCBF_EARLY_STORE ? u_out : nullptr, ep_pre, ep0);
