@@ -49,7 +49,10 @@ __device__ __forceinline__ int64_t env_index() {
 //   0 = plain stores (lines stay dirty in the XCD's L2 until the kernel-end
 //       write-back), 1 = write-through `sc1` stores (agent-scope relaxed
 //       atomic stores: the line leaves L2 as it is written), 2 = `nt` stores
-//       (default: with whole-line stores it is the fastest, profiles/r01).
+//       (default: with whole-line stores it is the fastest, profiles/r01),
+//       3 = the 16-byte stores (state pairs, staged observation chunks)
+//       write-through `sc1`, so their lines are not left dirty for the
+//       kernel-end L2 write-back; the narrow ones `nt`.
 #ifndef RCBF_STORE_MODE
 #define RCBF_STORE_MODE 2
 #endif
@@ -66,11 +69,19 @@ constexpr bool kObsNt = RCBF_OBS_NT;
 #define RCBF_EARLY_STORE 0
 #endif
 
+// one 16-byte write-through store: global_store_dwordx4 ... sc1 (the s_nop
+// covers the store-data hazard the compiler cannot see inside the asm)
+__device__ __forceinline__ void st_wt16(void* p, uint4 v) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const u4 w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+}
+
 template <typename T>
 __device__ __forceinline__ void st_out(T* p, T v) {
     if constexpr (kStoreMode == 1) {
         __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if constexpr (kStoreMode == 2) {
+    } else if constexpr (kStoreMode == 2 || kStoreMode == 3) {
         __builtin_nontemporal_store(v, p);
     } else {
         *p = v;
@@ -80,7 +91,9 @@ __device__ __forceinline__ void st_out(T* p, T v) {
 // 16-byte store (staged obs chunks), same flavours except sc1 -> plain
 __device__ __forceinline__ void st_out4(float* p, float4 v) {
     typedef float f4 __attribute__((ext_vector_type(4)));
-    if constexpr (kStoreMode == 2 && kObsNt) {
+    if constexpr (kStoreMode == 3) {
+        st_wt16(p, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)));
+    } else if constexpr (kStoreMode == 2 && kObsNt) {
         f4 w = {v.x, v.y, v.z, v.w};
         __builtin_nontemporal_store(w, reinterpret_cast<f4*>(p));
     } else {
@@ -94,6 +107,9 @@ __device__ __forceinline__ void st_out2d(double* p, double a, double b) {
     if constexpr (kStoreMode == 1) {
         st_out(p, a);
         st_out(p + 1, b);
+    } else if constexpr (kStoreMode == 3) {
+        const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
+        st_wt16(p, make_uint4((uint32_t)ua, (uint32_t)(ua >> 32), (uint32_t)ub, (uint32_t)(ub >> 32)));
     } else if constexpr (kStoreMode == 2) {
         d2 w = {a, b};
         __builtin_nontemporal_store(w, reinterpret_cast<d2*>(p));

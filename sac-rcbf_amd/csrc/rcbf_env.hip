@@ -194,6 +194,9 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B
     unsigned long long* stamps = nullptr;
 #endif
     RCBF_STAMP(stamps, 0, false);
+#ifdef RCBF_STAGGER  // performance study: odd workgroups start their loads later
+    if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(RCBF_STAGGER);
+#endif
     double xs[D::NS];
     load_state<MODE>(x, B, i, xs);
     double a = ld_in(&aux[i]);
