@@ -45,6 +45,24 @@ __device__ __forceinline__ double rcp64(double d) {
     return (d == 0.0) ? __builtin_copysign(__builtin_huge_val(), d) : r;
 }
 
+// The same two reciprocals without the d == 0 case (5 VALU fewer each; for
+// d = 0 they return NaN instead of inf).  For callers whose divisor is never
+// 0, or whose d = 0 result is discarded or multiplies a numerator that is 0
+// then too (0 * inf and 0 * NaN are both NaN): bit-identical results.
+__device__ __forceinline__ double rcp64_qp_nz(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
+__device__ __forceinline__ double rcp64_nz(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
 // ---------------------------------------------------------------------------
 // small fixed-size linear algebra (compile-time sizes -> registers)
 // (solver intermediates use rcp64: they are our own algorithm's quantities,
@@ -1023,15 +1041,15 @@ __device__ __forceinline__ void cars_qp_1d(const PMat<2, true>& pm, const R (*G)
     const double p0 = pm.P[0][0], p1 = pm.P[1][1];
     const double g00 = (double)G[0][0], g01 = (double)G[0][1], h0 = (double)h[0];
     const double g10 = (double)G[1][0], g11 = (double)G[1][1], h1 = (double)h[1];
-    const double U = (double)h[2] * rcp64_qp((double)G[2][0]);
-    const double L = (double)h[3] * rcp64_qp((double)G[3][0]);
-    const double i0 = rcp64_qp(g01), i1 = rcp64_qp(g11);
+    const double U = (double)h[2] * rcp64_qp_nz((double)G[2][0]);
+    const double L = (double)h[3] * rcp64_qp_nz((double)G[3][0]);
+    const double i0 = rcp64_qp_nz(g01), i1 = rcp64_qp_nz(g11);
     const double a0 = -g00 * i0, b0 = h0 * i0;  // e0(u) = a0 u + b0
     const double a1 = -g10 * i1, b1 = h1 * i1;  // e1(u) = a1 u + b1
-    const double c1 = -(p1 * a0 * b0) * rcp64_qp(fma(p1 * a0, a0, p0));
-    const double c2 = -(p1 * a1 * b1) * rcp64_qp(fma(p1 * a1, a1, p0));
+    const double c1 = -(p1 * a0 * b0) * rcp64_qp_nz(fma(p1 * a0, a0, p0));
+    const double c2 = -(p1 * a1 * b1) * rcp64_qp_nz(fma(p1 * a1, a1, p0));
     const double den = a0 - a1;
-    const double c3 = (den != 0.0) ? (b1 - b0) * rcp64_qp(den) : 0.0;
+    const double c3 = (den != 0.0) ? (b1 - b0) * rcp64_qp_nz(den) : 0.0;
     auto clampu = [&](double u) { return fmin(fmax(u, L), U); };
     auto phi = [&](double u) {
         double e = fmax(0.0, fmax(fma(a0, u, b0), fma(a1, u, b1)));
@@ -1084,16 +1102,16 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
     bool finite = true;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        const double inv = rcp64_qp((double)G[j][2]);
+        const double inv = rcp64_qp_nz((double)G[j][2]);
         a0[j] = -(double)G[j][0] * inv;
         a1[j] = -(double)G[j][1] * inv;
         b[j] = (double)h[j] * inv;
         finite = finite && isfinite(a0[j]) && isfinite(a1[j]) && isfinite(b[j]);
     }
-    const double U0 = (double)h[K] * rcp64_qp((double)G[K][0]);
-    const double L0 = (double)h[K + 1] * rcp64_qp((double)G[K + 1][0]);
-    const double U1 = (double)h[K + 2] * rcp64_qp((double)G[K + 2][1]);
-    const double L1 = (double)h[K + 3] * rcp64_qp((double)G[K + 3][1]);
+    const double U0 = (double)h[K] * rcp64_qp_nz((double)G[K][0]);
+    const double L0 = (double)h[K + 1] * rcp64_qp_nz((double)G[K + 1][0]);
+    const double U1 = (double)h[K + 2] * rcp64_qp_nz((double)G[K + 2][1]);
+    const double L1 = (double)h[K + 3] * rcp64_qp_nz((double)G[K + 3][1]);
     auto eps_of = [&](double u0, double u1) {
         double e = 0.0;
 #pragma unroll
@@ -1117,7 +1135,7 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
     for (int j = 0; j < K; ++j) {  // piece j: (diag(p0,p1) + p2 a a') u = -p2 b a
         double w0 = a0[j] * ip0, w1 = a1[j] * ip1;
         double sden = fma(p2, fma(a0[j], w0, a1[j] * w1), 1.0);
-        double f = -p2 * b[j] * rcp64_qp(sden);
+        double f = -p2 * b[j] * rcp64_qp_nz(sden);
         take(f * w0, f * w1);
     }
 #pragma unroll
@@ -1127,13 +1145,13 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
             double d0 = a0[i] - a0[j], d1 = a1[i] - a1[j], c = b[j] - b[i];
             double dd = fma(d0, d0, d1 * d1);
             if (dd > 1e-300) {
-                double idd = rcp64_qp(dd);
+                double idd = rcp64_qp_nz(dd);
                 double q0 = c * d0 * idd, q1 = c * d1 * idd;  // a point on the line
                 double n0 = -d1, n1 = d0;                     // its direction
                 double ea = fma(a0[i], q0, fma(a1[i], q1, b[i])), an = fma(a0[i], n0, a1[i] * n1);
                 double num = fma(p0 * q0, n0, fma(p1 * q1, n1, p2 * ea * an));
                 double den = fma(p0 * n0, n0, fma(p1 * n1, n1, p2 * an * an));
-                double t = -num * rcp64_qp(den);
+                double t = -num * rcp64_qp_nz(den);
                 take(fma(t, n0, q0), fma(t, n1, q1));
             }
         }
@@ -1148,7 +1166,7 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
                 double m10 = a0[i] - a0[l], m11 = a1[i] - a1[l], r1 = b[l] - b[i];
                 double det = fma(m00, m11, -m01 * m10);
                 if (fabs(det) > 1e-300) {
-                    double id = rcp64_qp(det);
+                    double id = rcp64_qp_nz(det);
                     take((r0 * m11 - r1 * m01) * id, (m00 * r1 - m10 * r0) * id);
                 }
             }
@@ -1183,13 +1201,13 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
             };
             cand(0.0);
 #pragma unroll
-            for (int j = 0; j < K; ++j) cand(-(p2 * al[j] * be[j]) * rcp64_qp(fma(p2 * al[j], al[j], pf)));
+            for (int j = 0; j < K; ++j) cand(-(p2 * al[j] * be[j]) * rcp64_qp_nz(fma(p2 * al[j], al[j], pf)));
 #pragma unroll
             for (int i = 0; i < K; ++i)
 #pragma unroll
                 for (int j = i + 1; j < K; ++j) {
                     double den = al[i] - al[j];
-                    if (den != 0.0) cand((be[j] - be[i]) * rcp64_qp(den));
+                    if (den != 0.0) cand((be[j] - be[i]) * rcp64_qp_nz(den));
                 }
         };
         edge(true, v0, L1, U1);
@@ -1253,7 +1271,9 @@ __device__ __forceinline__ void normalize_rows(T (*G)[N], T* h, T* Nrm, bool* ar
         Nrm[r] = nr;
         if (argmax_is_h) argmax_is_h[r] = ish;
         if constexpr (sizeof(T) == 4) {
-            const double rn = rcp64((double)nr);  // one reciprocal per row, exact fp32 quotients
+            // one reciprocal per row, exact fp32 quotients; nr = 0 only for an
+            // all-zero row, whose quotients are NaN either way (0 * inf, 0 * NaN)
+            const double rn = rcp64_nz((double)nr);
 #pragma unroll
             for (int k = 0; k < N; ++k) G[r][k] = div_f32_via_rcp(G[r][k], rn);
             h[r] = div_f32_via_rcp(h[r], rn);
