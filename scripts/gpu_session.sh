@@ -44,3 +44,16 @@ for step in "$@"; do
   esac
 done
 log "session done"
+# summarise the PMC passes on the box (the per-dispatch CSVs can be large)
+K='k_safe_step<0, 0, 1>'
+if [ -f "$OUT/pmc_fetch/run_counter_collection.csv" ] && [ -f "$OUT/pmc_write/run_counter_collection.csv" ]; then
+  python scripts/pmc_traffic.py "$OUT/pmc_fetch/run_counter_collection.csv" "$OUT/pmc_write/run_counter_collection.csv" \
+    "$K" "$OUT/pmc_traffic_cars_B65536.json" B=65536 env=SimulatedCars > /dev/null
+fi
+if [ -f "$OUT/pmc_fetch_u/run_counter_collection.csv" ] && [ -f "$OUT/pmc_write_u/run_counter_collection.csv" ]; then
+  python scripts/pmc_traffic.py "$OUT/pmc_fetch_u/run_counter_collection.csv" "$OUT/pmc_write_u/run_counter_collection.csv" \
+    'k_safe_step<0, 1, 3>' "$OUT/pmc_traffic_unicycle3_B65536.json" B=65536 env=Unicycle hazards=3 > /dev/null
+fi
+[ -f "$OUT/pmc_valu/run_counter_collection.csv" ] && python scripts/pmc_sq.py "$OUT/pmc_valu/run_counter_collection.csv" "$K" > "$OUT/pmc_sq_cars_B65536.txt"
+# keep what comes back under gpurun's 64 MiB cap: drop per-dispatch traces larger than 4 MiB
+find "$OUT" -type f -size +4M -print -delete
