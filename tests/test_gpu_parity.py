@@ -339,6 +339,51 @@ def test_fused_safe_step_unicycle(k):
     env.check_failures()
 
 
+@pytest.mark.parametrize("mode", ["SimulatedCars", "Unicycle"])
+def test_fused_step_ragged_batches_match_full_batch(mode):
+    """Ragged batches (a partial last wave, which stores its observations per
+    lane instead of through LDS) give bit-identical outputs to the same envs
+    inside a batch of whole waves; auto-resets included (episodes end here)."""
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+    Bf = 4160
+    rng = np.random.default_rng(31)
+    if mode == "SimulatedCars":
+        x, t, st = _cars_states(Bf, 32)
+        st = np.where(rng.random(Bf) < 0.3, 297, st)  # some episodes end during the test
+
+        def make(B):
+            e = BatchedSimulatedCarsEnv(B, seed=4)
+            e.load_state(x[:B], t[:B], st[:B])
+            return e
+    else:
+        hz = O.UNI["hazards"][:3]
+        x = np.stack([rng.uniform(-3, 3, Bf), rng.uniform(-3, 3, Bf), rng.uniform(-np.pi, np.pi, Bf)], 1)
+        st = np.where(rng.random(Bf) < 0.3, 997, 0)
+
+        def make(B):
+            e = BatchedUnicycleEnv(B, seed=4, hazards_locations=hz)
+            e.load_state(x[:B], O.uni_goal_dist(x[:B]), st[:B])
+            return e
+    full = make(Bf)
+    lf = _layer(full, 20.0)
+    us = [dev(rng.uniform(-1, 1, (Bf, full.n_u))) for _ in range(5)]
+    ref = []
+    for u in us:
+        obs, r, d, out = full.safe_step(u, lf)
+        ref.append([obs.clone(), r.clone(), d.clone(), out["u"].clone(), out["cost"].clone()])
+    for B in (1, 63, 65, 4133):
+        e = make(B)
+        le = _layer(e, 20.0)
+        for k, u in enumerate(us):
+            obs, r, d, out = e.safe_step(u[:B].contiguous(), le)
+            got = [obs, r, d, out["u"], out["cost"]]
+            for g, w in zip(got, ref[k]):
+                assert torch.equal(g, w[:B]), (B, k)
+        assert torch.equal(e.state, full.state[:B]) and torch.equal(e.step_count, full.step_count[:B])
+        e.check_failures()
+    assert int(full.episode.max().item()) >= 2  # auto-resets happened (construction counts as episode 1)
+
+
 def test_rollout_matches_single_steps():
     """K fused steps in one launch == K launches of the fused step."""
     from rcbf_amd.envs import BatchedSimulatedCarsEnv
