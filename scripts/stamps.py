@@ -20,7 +20,7 @@ class A:
 
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-uni = len(sys.argv) > 2 and sys.argv[2] == "unicycle"
+uni = "unicycle" in sys.argv[2:]
 if uni:
     hz = np.array([[0., 0.], [-1., 1.], [-1., -1.]]) * 1.5
     env = BatchedUnicycleEnv(B, seed=3, hazards_locations=hz)
@@ -39,13 +39,32 @@ lib = _lib.load()
 names = ["load", "get_state", "rows+norm", "QP", "env step", "obs+stores issued", "stores drained"]
 res = []
 fbs = []
-for rep in range(30):
-    st.zero_()
+graph = "--eager" not in sys.argv  # default: steady state inside a hipGraph replay, like bench.py
+
+
+def launch():
     rc = lib.rcbf_safe_step(ctypes.byref(layer._prm), B, _lib.ptr(env.x), _lib.ptr(env.aux), _lib.ptr(env.step_count),
                             _lib.ptr(env.episode), _lib.ptr(u), None, None, _lib.ptr(env.obs), _lib.ptr(o["u"]),
                             _lib.ptr(o["reward"]), _lib.ptr(o["cost"]), _lib.ptr(o["done"]), None, _lib.ptr(st),
                             None, 1, 1, 0, _lib.stream_of(torch.device("cuda")))
     assert rc == 0
+
+
+if graph:
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        launch()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(20):
+            launch()
+for rep in range(30):
+    if graph:
+        g.replay()  # the stamps of the last of 20 back-to-back steps
+    else:
+        st.zero_()
+        launch()
     torch.cuda.synchronize()
     if rep >= 10:
         t = st.view(nw, 16)[:, :8].cpu().numpy().astype(np.int64)
@@ -53,7 +72,7 @@ for rep in range(30):
         fb = st.view(nw, 16)[:, 9].cpu().numpy()
         fbs = fbs + [fb] if rep > 10 else [fb]
 d = np.concatenate(res)
-print(f"B={B}: per-phase s_memtime ticks per wave (median / p90), {d.shape[0]} wave samples")
+print(f"B={B} ({'hipGraph replay' if graph else 'eager'}): per-phase s_memtime ticks per wave (median / p90), {d.shape[0]} wave samples")
 for k, n in enumerate(names):
     print(f"  {n:20s} {np.median(d[:, k]):8.0f} {np.percentile(d[:, k], 90):8.0f}")
 fbv = np.concatenate(fbs)
