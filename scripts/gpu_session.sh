@@ -54,6 +54,8 @@ if [ -f "$OUT/pmc_fetch_u/run_counter_collection.csv" ] && [ -f "$OUT/pmc_write_
   python scripts/pmc_traffic.py "$OUT/pmc_fetch_u/run_counter_collection.csv" "$OUT/pmc_write_u/run_counter_collection.csv" \
     'k_safe_step<0, 1, 3>' "$OUT/pmc_traffic_unicycle3_B65536.json" B=65536 env=Unicycle hazards=3 > /dev/null
 fi
+[ -f "$OUT/prof/run_kernel_trace.csv" ] && python scripts/trace_summary.py "$OUT/prof/run_kernel_trace.csv" "$K" "$OUT/cars_B65536_kernel_trace_summary.json"
+[ -f "$OUT/profu/run_kernel_trace.csv" ] && python scripts/trace_summary.py "$OUT/profu/run_kernel_trace.csv" 'k_safe_step<0, 1, 3>' "$OUT/unicycle3_B65536_kernel_trace_summary.json"
 [ -f "$OUT/pmc_valu/run_counter_collection.csv" ] && python scripts/pmc_sq.py "$OUT/pmc_valu/run_counter_collection.csv" "$K" > "$OUT/pmc_sq_cars_B65536.txt"
 # keep what comes back under gpurun's 64 MiB cap: drop per-dispatch traces larger than 4 MiB
 find "$OUT" -type f -size +4M -print -delete
