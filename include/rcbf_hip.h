@@ -109,6 +109,19 @@ int rcbf_qp_solve(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const
                   float* z_out, double* lam_out, int32_t* status_out, int32_t* fail_flag,
                   hipStream_t stream);
 
+/* Backward of rcbf_qp_solve: CBFQPLayer.cbf_layer / solve_qp under autograd
+ * (diff_cbf_qp.py:81-144 -> qpth QPFunction.backward, diff_cbf_qp.py:139).
+ * Recomputes the exact forward in-kernel, then the implicit-KKT adjoint on
+ * the active set: grad_q = dz, grad_P = (dz z' + z dz')/2,
+ * grad_G = eta z' + lam dz', grad_h = -eta, pulled back through the row
+ * normaliser when normalize=1 (:103-106, torch.max/abs autograd rules).
+ * grad_z (B,n) in; grad_P (B,n,n), grad_q (B,n), grad_G (B,m,n),
+ * grad_h (B,m) out, each [nullable]; q [nullable] = 0. */
+int rcbf_qp_backward(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P,
+                     const float* q, const float* G, const float* h, int32_t normalize,
+                     const float* grad_z, float* grad_P, float* grad_q, float* grad_G,
+                     float* grad_h, hipStream_t stream);
+
 /* CBFQPLayer.get_safe_action (diff_cbf_qp.py:44-79), fused in one kernel:
  * build -> normalise -> fp64 QP -> .float() -> clamp(u_rl + u_qp, u_min, u_max).
  * mu/sigma [nullable] -> prior.  u_out (B, n_u) fp32. */

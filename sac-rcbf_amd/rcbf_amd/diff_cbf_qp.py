@@ -30,6 +30,14 @@ def _f32(t, dev):
     return t.detach().to(device=dev, dtype=torch.float32).contiguous()
 
 
+def _f32_keep_grad(t, dev):
+    """_f32 for inputs that may carry autograd history (kept differentiable)."""
+    if torch.is_tensor(t) and t.requires_grad:
+        t = t.to(device=dev, dtype=torch.float32)
+        return t if t.is_contiguous() else t.contiguous()
+    return _f32(t, dev)
+
+
 def _raise_if_failed(flag):
     bits = int(flag.item())  # one 4-byte read (the reference syncs here too, :141)
     if bits:
@@ -68,6 +76,44 @@ class _SafeAction(torch.autograd.Function):
                 _lib.ptr(g), _lib.ptr(gu), _lib.stream_of(x.device))
         _lib.check(rc, "rcbf_obs_safe_action_backward" if ctx.from_obs else "rcbf_safe_action_backward")
         return None, None, gu, None, None, None
+
+
+class _QP(torch.autograd.Function):
+    """z = QP(P, q, G, h) (optionally on row-normalised [G h]); backward is
+    rcbf_qp_backward: the implicit-KKT adjoint on the exact active set (what
+    qpth's QPFunction.backward approximates) w.r.t. P, q, G, h, pulled back
+    through the normaliser like torch autograd through diff_cbf_qp.py:103-106."""
+
+    @staticmethod
+    def forward(ctx, layer, normalize, P, q, G, h):
+        lib = _lib.load()
+        B, m, n = G.shape
+        z = torch.empty(B, n, device=G.device)
+        flag = torch.zeros(1, dtype=torch.int32, device=G.device)
+        rc = lib.rcbf_qp_solve(ctypes.byref(layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h),
+                               int(normalize), _lib.ptr(z), None, None, _lib.ptr(flag), _lib.stream_of(G.device))
+        _lib.check(rc, "rcbf_qp_solve")
+        _raise_if_failed(flag)
+        ctx.layer = layer
+        ctx.normalize = normalize
+        ctx.save_for_backward(P, q, G, h)
+        return z
+
+    @staticmethod
+    def backward(ctx, grad_z):
+        P, q, G, h = ctx.saved_tensors
+        B, m, n = G.shape
+        need = ctx.needs_input_grad
+        gz = grad_z.to(torch.float32).contiguous()
+        gP = torch.empty_like(P) if need[2] else None
+        gq = torch.empty(B, n, device=G.device) if (need[3] and q is not None) else None
+        gG = torch.empty_like(G) if need[4] else None
+        gh = torch.empty_like(h) if need[5] else None
+        rc = _lib.load().rcbf_qp_backward(ctypes.byref(ctx.layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G),
+                                          _lib.ptr(h), int(ctx.normalize), _lib.ptr(gz), _lib.ptr(gP), _lib.ptr(gq),
+                                          _lib.ptr(gG), _lib.ptr(gh), _lib.stream_of(G.device))
+        _lib.check(rc, "rcbf_qp_backward")
+        return None, None, gP, gq, gG, gh
 
 
 class CBFQPLayer:
@@ -162,21 +208,20 @@ class CBFQPLayer:
         return self._qp(Qs, ps, Gs, hs, normalize=False)
 
     def _qp(self, Ps, qs, Gs, hs, normalize):
-        if any(t.requires_grad for t in (Ps, qs, Gs, hs) if torch.is_tensor(t)):
-            raise NotImplementedError(
-                "gradients through cbf_layer/solve_qp directly are not provided; use get_safe_action, whose "
-                "backward covers the QP, the row normaliser and the clamp")
         dev = _dev()
-        P, G, h = _f32(Ps, dev), _f32(Gs, dev), _f32(hs, dev)
-        q = _f32(qs, dev) if qs is not None else None
+        G, h = _f32_keep_grad(Gs, dev), _f32_keep_grad(hs, dev)
+        if G.dim() != 3 or h.shape != G.shape[:2]:
+            raise ValueError(f"expected G (B,m,n) and h (B,m), got {tuple(G.shape)} / {tuple(h.shape)}")
         B, m, n = G.shape
-        z = torch.empty(B, n, device=dev)
-        flag = torch.zeros(1, dtype=torch.int32, device=dev)
-        rc = _lib.load().rcbf_qp_solve(ctypes.byref(self._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G),
-                                       _lib.ptr(h), int(normalize), _lib.ptr(z), None, None, _lib.ptr(flag),
-                                       _lib.stream_of(dev))
-        _lib.check(rc, "rcbf_qp_solve")
-        _raise_if_failed(flag)
+        P = _f32_keep_grad(Ps, dev)
+        if P.dim() == 2:  # qpth broadcasts an unbatched Q
+            P = P.expand(B, n, n).contiguous()
+        q = _f32_keep_grad(qs, dev) if qs is not None else None
+        if q is not None and q.dim() == 1:
+            q = q.expand(B, n).contiguous()
+        if P.shape != (B, n, n) or (q is not None and q.shape != (B, n)):
+            raise ValueError("P must be (B,n,n) and q (B,n)")
+        z = _QP.apply(self, bool(normalize), P, q, G, h)
         od = Gs.device if torch.is_tensor(Gs) else self.device
         return z.to(od)
 
