@@ -109,6 +109,13 @@ int rcbf_qp_solve(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const
                   float* z_out, double* lam_out, int32_t* status_out, int32_t* fail_flag,
                   hipStream_t stream);
 
+/* CascadeCBFLayer.solve_qp (cbf_qp.py:242-286, quadprog on the row-normalised
+ * problem): rcbf_qp_solve with fp64 inputs and an fp64 solution z_out (B,n). */
+int rcbf_qp_solve_f64(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const double* P,
+                      const double* q, const double* G, const double* h, int32_t normalize,
+                      double* z_out, double* lam_out, int32_t* status_out, int32_t* fail_flag,
+                      hipStream_t stream);
+
 /* Backward of rcbf_qp_solve: CBFQPLayer.cbf_layer / solve_qp under autograd
  * (diff_cbf_qp.py:81-144 -> qpth QPFunction.backward, diff_cbf_qp.py:139).
  * Recomputes the exact forward in-kernel, then the implicit-KKT adjoint on

@@ -1,31 +1,35 @@
 // rcbf_qp.hip -- generic QP and Cascade-layer kernels + C-ABI:
-// rcbf_qp_solve (CBFQPLayer.solve_qp / cbf_layer), rcbf_cascade_u_safe
-// (CascadeCBFLayer.get_u_safe).
+// rcbf_qp_solve / rcbf_qp_backward (CBFQPLayer.solve_qp / cbf_layer and their
+// autograd), rcbf_qp_solve_f64 (CascadeCBFLayer.solve_qp),
+// rcbf_cascade_u_safe (CascadeCBFLayer.get_u_safe).
 #include "rcbf_common.hpp"
 
 using namespace rcbf;
 
 namespace {
 
-// Generic QP (diff_cbf_qp.py:81-144): rows padded to MP with the never-active
-// row (0 z <= 1); general SPD P (n <= 3).
-template <int SOLVER, int N, int MP>
-__global__ void __launch_bounds__(kBlock) k_qp_solve(rcbf_params prm, int64_t B, int m, const float* __restrict__ P,
-                                                     const float* __restrict__ q, const float* __restrict__ G,
-                                                     const float* __restrict__ h, int normalize,
-                                                     float* __restrict__ z_out, double* __restrict__ lam_out,
+// Generic QP (diff_cbf_qp.py:81-144; fp64 inputs: CascadeCBFLayer.solve_qp,
+// cbf_qp.py:242-286): rows padded to MP with the never-active row
+// (0 z <= 1); general SPD P (n <= 3).  T = float: the fp32 rows of the diff
+// layer (z returned as fp32, the reference's .float()); T = double: fp64
+// throughout.
+template <int SOLVER, int N, int MP, typename T>
+__global__ void __launch_bounds__(kBlock) k_qp_solve(rcbf_params prm, int64_t B, int m, const T* __restrict__ P,
+                                                     const T* __restrict__ q, const T* __restrict__ G,
+                                                     const T* __restrict__ h, int normalize,
+                                                     T* __restrict__ z_out, double* __restrict__ lam_out,
                                                      int32_t* __restrict__ status_out, int32_t* fail_flag) {
     int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= B) return;
-    float Gl[MP][N], hl[MP], Nrm[MP];
+    T Gl[MP][N], hl[MP], Nrm[MP];
 #pragma unroll
     for (int r = 0; r < MP; ++r) {
         bool in = r < m;
 #pragma unroll
-        for (int k = 0; k < N; ++k) Gl[r][k] = in ? G[(i * m + r) * N + k] : 0.0f;
-        hl[r] = in ? h[i * m + r] : 1.0f;
+        for (int k = 0; k < N; ++k) Gl[r][k] = in ? G[(i * m + r) * N + k] : T(0);
+        hl[r] = in ? h[i * m + r] : T(1);
     }
-    if (normalize) normalize_rows<N, MP, float>(Gl, hl, Nrm, nullptr);
+    if (normalize) normalize_rows<N, MP, T>(Gl, hl, Nrm, nullptr);
     double Pin[N][N], qd[N];
 #pragma unroll
     for (int a = 0; a < N; ++a) {
@@ -36,9 +40,9 @@ __global__ void __launch_bounds__(kBlock) k_qp_solve(rcbf_params prm, int64_t B,
     PMat<N, false> pm;
     pmat_set_full<N>(pm, Pin);
     QPResult<N, MP> res;
-    qp_solve<SOLVER, N, MP, false, float>(pm, qd, Gl, hl, prm.max_iter, prm.eps, res);
+    qp_solve<SOLVER, N, MP, false, T>(pm, qd, Gl, hl, prm.max_iter, prm.eps, res);
 #pragma unroll
-    for (int k = 0; k < N; ++k) z_out[i * N + k] = (float)res.z[k];
+    for (int k = 0; k < N; ++k) z_out[i * N + k] = (T)res.z[k];
     if (lam_out) {
 #pragma unroll
         for (int r = 0; r < MP; ++r)
@@ -243,13 +247,10 @@ __global__ void __launch_bounds__(kBlock) k_cascade(rcbf_params prm, int64_t B, 
     report(res.status, status_out, i, fail_flag);
 }
 
-}  // namespace
-
-extern "C" {
-
-int rcbf_qp_solve(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P, const float* q,
-                  const float* G, const float* h, int32_t normalize, float* z_out, double* lam_out,
-                  int32_t* status_out, int32_t* fail_flag, hipStream_t stream) {
+template <typename T>
+int qp_solve_launch(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const T* P, const T* q, const T* G,
+                    const T* h, int32_t normalize, T* z_out, double* lam_out, int32_t* status_out,
+                    int32_t* fail_flag, hipStream_t stream) {
     if (!prm) return RCBF_E_NULL;
     if (prm->solver != RCBF_SOLVER_ACTIVE_SET && prm->solver != RCBF_SOLVER_PDIPM && prm->solver != RCBF_SOLVER_GI)
         return RCBF_E_BAD_MODE;
@@ -257,14 +258,14 @@ int rcbf_qp_solve(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const
     if (B == 0) return 0;
     if (!P || !G || !h || !z_out) return RCBF_E_NULL;
     dim3 g(grid_for(B)), b(kBlock);
-#define RCBF_QP_L(NN, MP)                                                                                         \
-    do {                                                                                                          \
-        if (prm->solver == RCBF_SOLVER_PDIPM)                                                                     \
-            hipLaunchKernelGGL((k_qp_solve<RCBF_SOLVER_PDIPM, NN, MP>), g, b, 0, stream, *prm, B, m, P, q, G, h, \
-                               normalize, z_out, lam_out, status_out, fail_flag);                                 \
-        else                                                                                                      \
-            hipLaunchKernelGGL((k_qp_solve<RCBF_SOLVER_GI, NN, MP>), g, b, 0, stream, *prm, B, m, P, q, G, h,    \
-                               normalize, z_out, lam_out, status_out, fail_flag);                                 \
+#define RCBF_QP_L(NN, MP)                                                                                      \
+    do {                                                                                                       \
+        if (prm->solver == RCBF_SOLVER_PDIPM)                                                                  \
+            hipLaunchKernelGGL((k_qp_solve<RCBF_SOLVER_PDIPM, NN, MP, T>), g, b, 0, stream, *prm, B, m, P, q, \
+                               G, h, normalize, z_out, lam_out, status_out, fail_flag);                        \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_qp_solve<RCBF_SOLVER_GI, NN, MP, T>), g, b, 0, stream, *prm, B, m, P, q, G, \
+                               h, normalize, z_out, lam_out, status_out, fail_flag);                           \
     } while (0)
 #define RCBF_QP_M(NN)           \
     do {                        \
@@ -286,6 +287,23 @@ int rcbf_qp_solve(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const
 #undef RCBF_QP_M
 #undef RCBF_QP_L
     return launch_status();
+}
+
+}  // namespace
+
+extern "C" {
+
+int rcbf_qp_solve(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P, const float* q,
+                  const float* G, const float* h, int32_t normalize, float* z_out, double* lam_out,
+                  int32_t* status_out, int32_t* fail_flag, hipStream_t stream) {
+    return qp_solve_launch<float>(prm, B, n, m, P, q, G, h, normalize, z_out, lam_out, status_out, fail_flag, stream);
+}
+
+int rcbf_qp_solve_f64(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const double* P, const double* q,
+                      const double* G, const double* h, int32_t normalize, double* z_out, double* lam_out,
+                      int32_t* status_out, int32_t* fail_flag, hipStream_t stream) {
+    return qp_solve_launch<double>(prm, B, n, m, P, q, G, h, normalize, z_out, lam_out, status_out, fail_flag,
+                                   stream);
 }
 
 int rcbf_qp_backward(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P, const float* q,

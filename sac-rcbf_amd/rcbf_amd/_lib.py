@@ -71,6 +71,7 @@ SIGNATURES = {
     "rcbf_build": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_build_f64": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_qp_solve": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P],
+    "rcbf_qp_solve_f64": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "rcbf_qp_backward": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P],
     "rcbf_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],

@@ -77,14 +77,58 @@ class CascadeCBFLayer:
             return P[0], q[0], G[0], h[0]
         return P, q, G, h
 
+    def solve_qp(self, P, q, G, h):
+        """cbf_qp.py:242-286: normalise the rows of [G h] (G in place, like the
+        reference's `G /= Gh_norm`), solve min 1/2 z'Pz + q'z s.t. Gz <= h
+        exactly in fp64 (rcbf_qp_solve_f64, Goldfarb-Idnani as quadprog) and
+        return z without the slack.  Infeasible -> quadprog's ValueError."""
+        if not torch.cuda.is_available():
+            raise RuntimeError("CascadeCBFLayer needs a HIP device (MI355X); there is no CPU fallback")
+        Gh = np.concatenate((G, np.expand_dims(h, 1)), 1)
+        Gh_norm = np.expand_dims(np.max(np.abs(Gh), axis=1), axis=1)
+        G /= Gh_norm  # the caller's G, in place as :272
+        h = h / Gh_norm.squeeze(-1)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        m, n = np.shape(G)
+
+        def d(a):
+            return torch.as_tensor(np.asarray(a, np.float64).reshape(1, -1), device=dev).contiguous()
+
+        Pd, qd, Gd, hd = d(P), d(q), d(G), d(h)
+        z = torch.empty(1, n, dtype=torch.float64, device=dev)
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        rc = _lib.load().rcbf_qp_solve_f64(ctypes.byref(self._prm), 1, n, m, _lib.ptr(Pd), _lib.ptr(qd), _lib.ptr(Gd),
+                                           _lib.ptr(hd), 0, _lib.ptr(z), None, None, _lib.ptr(flag),
+                                           _lib.stream_of(dev))
+        _lib.check(rc, "rcbf_qp_solve_f64")
+        if int(flag.item()):
+            raise ValueError("constraints are inconsistent, no solution")
+        return z[0, :-1].cpu().numpy()
+
+    def get_cbfs(self, hazards_locations, hazards_radius):
+        """cbf_qp.py:288-323: (get_h, get_dhdx) of the hazard CBFs
+        h_j(s) = 1/2 (||p(s) - o_j||^2 - (r + 0.07)^2) on the look-ahead output
+        p(s) (unicycle) or the state itself."""
+        hz = np.array(hazards_locations)
+        r = hazards_radius + 0.07
+
+        def out(state):
+            if self.env.dynamics_mode == "Unicycle":
+                return np.array([state[0] + self.l_p * np.cos(state[2]), state[1] + self.l_p * np.sin(state[2])])
+            return state
+
+        def get_h(state):
+            return 0.5 * (np.sum((out(state) - hz) ** 2, axis=1) - r ** 2)
+
+        def get_dhdx(state):
+            return out(state) - hz
+
+        return get_h, get_dhdx
+
     def get_control_bounds(self):
         return self.env.safe_action_space.low, self.env.safe_action_space.high
 
     def get_min_h_val(self, state):
-        """cbf_qp.py:341-358 (uses the r + 0.07 radius of get_cbfs :308)."""
-        hz = np.asarray(self.env.hazards_locations)
-        r = self.env.hazards_radius + 0.07
-        st = np.asarray(state, np.float64)
-        if self.env.dynamics_mode == "Unicycle":
-            st = np.array([st[0] + self.l_p * np.cos(st[2]), st[1] + self.l_p * np.sin(st[2])])
-        return np.min(0.5 * (np.sum((st - hz) ** 2, axis=1) - r ** 2))
+        """cbf_qp.py:341-358."""
+        get_h, _ = self.get_cbfs(self.env.hazards_locations, self.env.hazards_radius)
+        return np.min(get_h(state))

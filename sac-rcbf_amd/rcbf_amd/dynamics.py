@@ -72,6 +72,47 @@ class DynamicsModel:
         self.train_x = np.array(train_x, copy=True)
         self.train_y = np.array(train_y, copy=True)
 
+    # -- GP persistence and seeding (dynamics.py:392-425; main.py:136,183,313) --
+    def save_disturbance_models(self, output):
+        """Writes gp_models.pkl (per state dim: lengthscale, outputscale,
+        noise) and the training data gp_models_train_x/_y.pkl under `output`
+        -- the reference's file names; tensors only, so they load with
+        torch.load(weights_only=True).  The hyperparameters are stored as
+        values, not as a gpytorch state_dict (gpytorch is not used here)."""
+        if not self.disturb_estimators or self.train_x is None or self.train_y is None:
+            return
+        weights = [{"lengthscale": torch.tensor(h[0], dtype=torch.float64),
+                    "outputscale": torch.tensor(h[1], dtype=torch.float64),
+                    "noise": torch.tensor(h[2], dtype=torch.float64)} for h in self.disturb_estimators.hyper]
+        torch.save(weights, f"{output}/gp_models.pkl")
+        torch.save(torch.as_tensor(self.train_x), f"{output}/gp_models_train_x.pkl")
+        torch.save(torch.as_tensor(self.train_y), f"{output}/gp_models_train_y.pkl")
+
+    def load_disturbance_models(self, output):
+        """Restores what save_disturbance_models wrote (None -> no-op); any
+        failure raises Exception('Could not load GP models from ...') like the
+        reference."""
+        if output is None:
+            return
+        from . import gp
+        self.disturb_estimators = None
+        try:
+            weights = torch.load(f"{output}/gp_models.pkl", weights_only=True)
+            tx = torch.load(f"{output}/gp_models_train_x.pkl", weights_only=True).cpu().numpy()
+            ty = torch.load(f"{output}/gp_models_train_y.pkl", weights_only=True).cpu().numpy()
+            hyper = [(float(w["lengthscale"]), float(w["outputscale"]), float(w["noise"])) for w in weights]
+            if len(hyper) != self.n_s:
+                raise ValueError("state dimension mismatch")
+            self.disturb_estimators = gp.GPDisturbanceModel(tx, ty, hyper, rank=self.gp_rank)
+            self.train_x, self.train_y = tx, ty
+        except Exception:
+            raise Exception("Could not load GP models from {}".format(output))
+
+    def seed(self, s):
+        torch.manual_seed(s)
+        if torch.cuda.is_available():
+            torch.cuda.manual_seed(s)
+
     # -- obs <-> state (dynamics.py:190-261) -------------------------------
     def get_state(self, obs):
         expand = len(obs.shape) == 1
@@ -148,6 +189,33 @@ class DynamicsModel:
         if t_batch is not None:
             return nxt, dt * std, t_batch + dt
         return nxt, dt * std, t_batch
+
+    def predict_next_obs(self, state, u):
+        """dynamics.py:107-123: the mean next observation."""
+        next_state, _, _ = self.predict_next_state(state, u)
+        return self.get_obs(next_state)
+
+    def get_dynamics(self):
+        """dynamics.py:125-188: (get_f, get_g) of the model prior x' = f(x) + g(x) u
+        on numpy (B, n_s) batches; g is (B, n_s, n_u)."""
+        n_s, n_u = self.n_s, self.n_u
+
+        def get_f(state_batch, t_batch=None):
+            x = np.asarray(state_batch, np.float64)
+            return self._f_plus_gu(x, np.zeros((x.shape[0], n_u)), t_batch)
+
+        def get_g(state_batch, t_batch=None):
+            x = np.asarray(state_batch, np.float64)
+            g = np.zeros((x.shape[0], n_s, n_u))
+            if self.env.dynamics_mode == "Unicycle":
+                g[:, 0, 0] = np.cos(x[:, 2])
+                g[:, 1, 0] = np.sin(x[:, 2])
+                g[:, 2, 1] = 1.0
+            else:
+                g[:, 7, 0] = 50.0
+            return g
+
+        return get_f, get_g
 
     def _f_plus_gu(self, x, u, t_batch):
         """f(x) + g(x) u of the model prior (dynamics.py:125-188)."""

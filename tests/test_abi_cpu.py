@@ -108,3 +108,22 @@ def test_state_pair_layout_roundtrip():
         assert torch.equal(pairs_to_rows(xf, n_s, B), rows)
         if B == 1:
             assert torch.equal(xf, rows[0])
+
+
+def test_cascade_get_cbfs_and_min_h():
+    """CascadeCBFLayer.get_cbfs / get_min_h_val (cbf_qp.py:288-358): host
+    numpy helpers, radius + 0.07 buffer, look-ahead output for the unicycle."""
+    import numpy as np
+    from rcbf_amd.cbf_qp import CascadeCBFLayer
+    from rcbf_amd.envs import _EnvSpec
+    env = _EnvSpec("Unicycle")
+    cl = CascadeCBFLayer(env, l_p=0.03)
+    get_h, get_dhdx = cl.get_cbfs(env.hazards_locations, env.hazards_radius)
+    s = np.array([0.5, -0.2, 0.7])
+    p = np.array([s[0] + 0.03 * np.cos(s[2]), s[1] + 0.03 * np.sin(s[2])])
+    hz = np.asarray(env.hazards_locations)
+    assert np.allclose(get_h(s), 0.5 * (((p - hz) ** 2).sum(1) - 0.67 ** 2), rtol=0, atol=1e-15)
+    assert np.allclose(get_dhdx(s), p - hz, rtol=0, atol=1e-15)
+    assert cl.get_min_h_val(s) == np.min(get_h(s))
+    centre = np.array([hz[0, 0] - 0.03, hz[0, 1], 0.0])
+    assert abs(cl.get_min_h_val(centre) + 0.5 * 0.67 ** 2) < 1e-12

@@ -99,3 +99,35 @@ def test_append_transition_disturbance():
     assert calls == [10, 20] and dm.history_counter == 25
     assert np.allclose(dm.disturbance_history["disturbance"][:25], d_true, atol=1e-12)
     assert np.array_equal(dm.disturbance_history["state"][:25], x)
+
+
+def test_get_dynamics_and_predict_next_obs(golden):
+    """dynamics.py:107-188: get_dynamics' (f, g) rebuild the golden prior step
+    x + dt (f + g u) (as the reference's predict_next_state uses them), and
+    predict_next_obs = get_obs(predict_next_state(...))."""
+    d = golden("dynamics")
+    for nm, mode in (("cars", "SimulatedCars"), ("uni", "Unicycle")):
+        dm = _dyn(mode)
+        x, u, t = d[nm + "_state_np"], d[nm + "_u"], d.get(nm + "_t")
+        get_f, get_g = dm.get_dynamics()
+        g = get_g(x, t)
+        assert g.shape == (x.shape[0], dm.n_s, dm.n_u)
+        nx = x + 0.02 * (get_f(x, t) + np.einsum("bsu,bu->bs", g, u))
+        assert np.array_equal(nx, d[nm + "_next"])
+    dm = _dyn("Unicycle")
+    x = d["uni_state_np"]; u = d["uni_u"]
+    assert np.array_equal(dm.predict_next_obs(x, u), dm.get_obs(dm.predict_next_state(x, u)[0]))
+
+
+def test_seed_and_load_none():
+    """seed() seeds torch like dynamics.py:421-424; load_disturbance_models(None)
+    is a no-op and a missing directory raises the reference's message."""
+    dm = _dyn("Unicycle")
+    dm.seed(5)
+    a = torch.rand(3)
+    dm.seed(5)
+    assert torch.equal(a, torch.rand(3))
+    dm.load_disturbance_models(None)
+    assert dm.disturb_estimators is None
+    with pytest.raises(Exception, match="Could not load GP models from /nonexistent"):
+        dm.load_disturbance_models("/nonexistent")

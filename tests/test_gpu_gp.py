@@ -85,3 +85,24 @@ def test_dynamics_model_gp_fit_and_safe_action():
     out = get_safe_action(layer, torch.as_tensor(obs, device="cuda"), torch.as_tensor(ua, device="cuda"), dm)
     fin, _ = O.safe_action_diff("Unicycle", s32, ua, mean.cpu().numpy(), std.cpu().numpy(), 20.0, hazards=hz)
     assert np.max(np.abs(out.cpu().numpy() - fin)) <= 1e-4
+
+
+def test_save_load_disturbance_models_round_trip(tmp_path):
+    """main.py:136,183: save_disturbance_models then load_disturbance_models in
+    a fresh DynamicsModel restores the same GP posterior (bit-equal)."""
+    from rcbf_amd.dynamics import DynamicsModel
+    env = types.SimpleNamespace(dynamics_mode="Unicycle", dt=0.02)
+    args = types.SimpleNamespace(cuda=True, gp_model_size=200)
+    dm = DynamicsModel(env, args)
+    rng = np.random.default_rng(4)
+    x = rng.normal(0, 1, (200, 3)); u = rng.uniform(-1, 1, (200, 2))
+    nx = O.predict_next_state_prior("Unicycle", x, u) + 0.02 * (0.05 * np.sin(x) + rng.normal(0, 0.02, x.shape))
+    dm.append_transition(x, u, nx)
+    q = torch.as_tensor(rng.normal(0, 1, (64, 3)), dtype=torch.float32, device="cuda")
+    m0, s0 = dm.predict_disturbance(q)
+    dm.save_disturbance_models(str(tmp_path))
+    dm2 = DynamicsModel(env, args)
+    dm2.load_disturbance_models(str(tmp_path))
+    m1, s1 = dm2.predict_disturbance(q)
+    assert torch.equal(m0, m1) and torch.equal(s0, s1)
+    assert dm2.disturb_estimators.hyper == dm.disturb_estimators.hyper

@@ -180,6 +180,28 @@ def test_cascade_golden(golden):
     assert one.shape == (2,) and rel(one, c["uni_usafe"][0]) <= 1e-7
 
 
+def test_cascade_solve_qp_golden(golden):
+    """CascadeCBFLayer.solve_qp (cbf_qp.py:242-286) on the reference's own
+    rows: the exact fp64 solution (quadprog's), the caller's G normalised in
+    place, and quadprog's ValueError on an infeasible QP."""
+    from rcbf_amd.cbf_qp import CascadeCBFLayer
+    from rcbf_amd.envs import SimulatedCarsEnv, UnicycleEnv
+    c = golden("cascade")
+    for layer, nm, tol in ((CascadeCBFLayer(SimulatedCarsEnv(), gamma_b=20.0, k_d=3.0), "cars", 1e-9),
+                           (CascadeCBFLayer(UnicycleEnv(), gamma_b=40.0, k_d=3.0, l_p=0.03), "uni", 1e-7)):
+        P = c[nm + "_P"]
+        for b in range(0, 256, 8):
+            G, h = c[nm + "_G"][b].copy(), c[nm + "_h"][b]
+            u = layer.solve_qp(P, np.zeros(P.shape[0]), G, h)
+            assert u.shape == (P.shape[0] - 1,)
+            assert rel(u, c[nm + "_usafe"][b]) <= tol
+            Gn, _, _ = O.normalize_rows(c[nm + "_G"][b][None], h[None])
+            assert np.array_equal(G, Gn[0])
+    G = np.array([[1.0, 0.0], [-1.0, 0.0]])
+    with pytest.raises(ValueError):
+        layer.solve_qp(np.eye(2), np.zeros(2), G, np.array([-1.0, -1.0]))
+
+
 # ----------------------------------------------------------------------------
 # environments vs reference trajectories
 # ----------------------------------------------------------------------------
