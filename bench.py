@@ -342,6 +342,48 @@ def sac_update_safe_action(env, layer, dev):
     return res
 
 
+def generic_qp_rows(layer, dev):
+    """CBFQPLayer.solve_qp / cbf_layer under autograd (rcbf_qp_solve +
+    rcbf_qp_backward, diff_cbf_qp.py:81-144) on the layer's own rows:
+    cars-shaped (n = 2, m = 4) and unicycle-shaped (n = 3, m = 7) QPs, full
+    P, row-normalised; forward and backward launch times from one hipGraph,
+    with the algorithmic bytes per QP (fwd: P, q, G, h in + z out; bwd: the
+    same in + grad_z in + grad_P, grad_q, grad_G, grad_h out)."""
+    import ctypes
+    from rcbf_amd import _lib
+    lib = _lib.load()
+    out = {}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    for n, m in ((2, 4), (3, 7)):
+        for B in (4096, 65536):
+            A = torch.randn(B, n, n, device=dev, generator=gen)
+            P = (A @ A.transpose(1, 2) + n * torch.eye(n, device=dev)).contiguous()
+            q = torch.randn(B, n, device=dev, generator=gen)
+            G = torch.randn(B, m, n, device=dev, generator=gen)
+            z0 = 0.3 * torch.randn(B, n, device=dev, generator=gen)
+            h = (torch.einsum("bmn,bn->bm", G, z0) + 0.5 * torch.randn(B, m, device=dev, generator=gen).abs()).contiguous()
+            z = torch.empty(B, n, device=dev)
+            gz = torch.randn(B, n, device=dev, generator=gen)
+            gP, gq, gG, gh = torch.empty_like(P), torch.empty_like(q), torch.empty_like(G), torch.empty_like(h)
+            prm = ctypes.byref(layer._prm)
+
+            def fwd():
+                lib.rcbf_qp_solve(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(z),
+                                  None, None, None, _lib.stream_of(dev))
+
+            def bwd():
+                lib.rcbf_qp_backward(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(gz),
+                                     _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh), _lib.stream_of(dev))
+            by_in = 4 * (n * n + n + m * n + m)
+            fms, bms = _time_graph(fwd, 20, dev), _time_graph(bwd, 20, dev)
+            out[f"qp_n{n}_m{m}_B{B}"] = {
+                "fwd_us": round(fms * 1e3, 2), "bwd_us": round(bms * 1e3, 2),
+                "fwd_GBs": round(B * (by_in + 4 * n) / fms / 1e6, 1),
+                "bwd_GBs": round(B * (2 * by_in + 4 * n) / bms / 1e6, 1)}
+    return out
+
+
 def _time_graph(fn, reps, dev):
     """Mean ms per fn() call, fn captured `reps` times in one hipGraph."""
     s = torch.cuda.Stream(device=dev)
@@ -431,6 +473,7 @@ def extra_measurements(env, layer, dev, args):
     ms = e0.elapsed_time(e1)
     out["rollout_K100_steps_per_s"] = round(env.num_envs * K / (ms * 1e-3), 1)
     out.update(sac_update_safe_action(env, layer, dev))
+    out.update(generic_qp_rows(layer, dev))
     out.update(next_rows(dev))
     if args.env == "SimulatedCars":
         Bb = 4 * 1024 * 1024
