@@ -1128,7 +1128,7 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
         bool t = f < bf;  // NaN candidates never win
         bu0 = t ? u0 : bu0;
         bu1 = t ? u1 : bu1;
-        bf = t ? f : bf;
+        bf = fmin(bf, f);  // = t ? f : bf (fmin drops a NaN f)
     };
     // stage 1: box-free candidates
 #pragma unroll
@@ -1143,17 +1143,16 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
 #pragma unroll
         for (int j = i + 1; j < K; ++j) {  // kink line (a_i - a_j).u = b_j - b_i, minimise along it
             double d0 = a0[i] - a0[j], d1 = a1[i] - a1[j], c = b[j] - b[i];
+            // parallel pieces (dd = 0) give NaN through rcp64_qp_nz and never win
             double dd = fma(d0, d0, d1 * d1);
-            if (dd > 1e-300) {
-                double idd = rcp64_qp_nz(dd);
-                double q0 = c * d0 * idd, q1 = c * d1 * idd;  // a point on the line
-                double n0 = -d1, n1 = d0;                     // its direction
-                double ea = fma(a0[i], q0, fma(a1[i], q1, b[i])), an = fma(a0[i], n0, a1[i] * n1);
-                double num = fma(p0 * q0, n0, fma(p1 * q1, n1, p2 * ea * an));
-                double den = fma(p0 * n0, n0, fma(p1 * n1, n1, p2 * an * an));
-                double t = -num * rcp64_qp_nz(den);
-                take(fma(t, n0, q0), fma(t, n1, q1));
-            }
+            double idd = rcp64_qp_nz(dd);
+            double q0 = c * d0 * idd, q1 = c * d1 * idd;  // a point on the line
+            double n0 = -d1, n1 = d0;                     // its direction
+            double ea = fma(a0[i], q0, fma(a1[i], q1, b[i])), an = fma(a0[i], n0, a1[i] * n1);
+            double num = fma(p0 * q0, n0, fma(p1 * q1, n1, p2 * ea * an));
+            double den = fma(p0 * n0, n0, fma(p1 * n1, n1, p2 * an * an));
+            double t = -num * rcp64_qp_nz(den);
+            take(fma(t, n0, q0), fma(t, n1, q1));
         }
     }
 #pragma unroll
@@ -1165,10 +1164,8 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
                 double m00 = a0[i] - a0[j], m01 = a1[i] - a1[j], r0 = b[j] - b[i];
                 double m10 = a0[i] - a0[l], m11 = a1[i] - a1[l], r1 = b[l] - b[i];
                 double det = fma(m00, m11, -m01 * m10);
-                if (fabs(det) > 1e-300) {
-                    double id = rcp64_qp_nz(det);
-                    take((r0 * m11 - r1 * m01) * id, (m00 * r1 - m10 * r0) * id);
-                }
+                double id = rcp64_qp_nz(det);  // det = 0: NaN, never wins
+                take((r0 * m11 - r1 * m01) * id, (m00 * r1 - m10 * r0) * id);
             }
         }
     }
@@ -1197,7 +1194,7 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
                 const bool t = f < bf;
                 bu0 = t ? (fix0 ? v : y) : bu0;
                 bu1 = t ? (fix0 ? y : v) : bu1;
-                bf = t ? f : bf;
+                bf = fmin(bf, f);
             };
             cand(0.0);
 #pragma unroll
@@ -1206,8 +1203,9 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
             for (int i = 0; i < K; ++i)
 #pragma unroll
                 for (int j = i + 1; j < K; ++j) {
+                    // den = 0: NaN, which the clamp in cand turns into the feasible point lo
                     double den = al[i] - al[j];
-                    if (den != 0.0) cand((be[j] - be[i]) * rcp64_qp_nz(den));
+                    cand((be[j] - be[i]) * rcp64_qp_nz(den));
                 }
         };
         edge(true, v0, L1, U1);
