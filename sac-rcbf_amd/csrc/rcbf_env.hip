@@ -174,8 +174,17 @@ __global__ void __launch_bounds__(kBlock) k_env_step(rcbf_params prm, int64_t B,
     if (obs32) store_obs32<MODE>(obs32, i, xs);
 }
 
+// Performance study: RCBF_WAVES_PER_EU=n tells the register allocator and the
+// scheduler that n waves per SIMD suffice (the fused step runs one wave per
+// SIMD at B = 65536), trading occupancy for instruction-level parallelism.
+#ifdef RCBF_WAVES_PER_EU
+#define RCBF_STEP_ATTR __attribute__((amdgpu_waves_per_eu(RCBF_WAVES_PER_EU, RCBF_WAVES_PER_EU)))
+#else
+#define RCBF_STEP_ATTR
+#endif
+
 template <int SOLVER, int MODE, int K>
-__global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B, double* __restrict__ x,
+__global__ void __launch_bounds__(kBlock) RCBF_STEP_ATTR k_safe_step(rcbf_params prm, int64_t B, double* __restrict__ x,
                                                       double* __restrict__ aux, int32_t* __restrict__ step,
                                                       uint32_t* __restrict__ episode, const float* __restrict__ u_rl,
                                                       const float* __restrict__ mu, const float* __restrict__ sigma,

@@ -38,9 +38,21 @@ def _f32_keep_grad(t, dev):
     return _f32(t, dev)
 
 
+def _fail_flag(layer, device):
+    """The layer's persistent device fail-flag word for `device` (zero between
+    calls: a call that sees it set clears it before raising), so a call costs
+    no fill launch."""
+    flags = layer.__dict__.setdefault("_fail_flags", {})
+    f = flags.get(device)
+    if f is None:
+        f = flags[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    return f
+
+
 def _raise_if_failed(flag):
     bits = int(flag.item())  # one 4-byte read (the reference syncs here too, :141)
     if bits:
+        flag.zero_()
         raise Exception(_QP_FAILED)
 
 
@@ -53,7 +65,7 @@ class _SafeAction(torch.autograd.Function):
         lib = _lib.load()
         B = x.shape[0]
         out = torch.empty_like(u)
-        flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+        flag = _fail_flag(layer, x.device) if layer.check_failures else None
         fn = lib.rcbf_obs_safe_action if from_obs else lib.rcbf_safe_action
         rc = fn(ctypes.byref(layer._prm), B, _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu), _lib.ptr(sigma),
                 _lib.ptr(out), None, _lib.ptr(flag), _lib.stream_of(x.device))
@@ -89,7 +101,7 @@ class _QP(torch.autograd.Function):
         lib = _lib.load()
         B, m, n = G.shape
         z = torch.empty(B, n, device=G.device)
-        flag = torch.zeros(1, dtype=torch.int32, device=G.device)
+        flag = _fail_flag(layer, G.device)
         rc = lib.rcbf_qp_solve(ctypes.byref(layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h),
                                int(normalize), _lib.ptr(z), None, None, _lib.ptr(flag), _lib.stream_of(G.device))
         _lib.check(rc, "rcbf_qp_solve")

@@ -305,14 +305,43 @@ class _SingleEnv(_EnvBase):
         return self
 
     def step(self, action):
+        """One env step with ONE device->host transfer: the kernel writes
+        obs (fp64), reward, cost, done and goal_met into one packed device
+        row, which is copied to pinned host memory and synchronised once (the
+        action goes up through a pinned buffer without a sync)."""
         a = np.asarray(action)
         if a.dtype not in (np.float32, np.float64):
             a = a.astype(np.float32)
-        obs32, reward, done, info = self._b.step(torch.as_tensor(a.reshape(1, -1)), auto_reset=False, obs64=True)
-        obs = info["obs64"][0].cpu().numpy()
-        r = reward[0].item()
-        r = np.float32(r) if a.dtype == np.float32 else np.float64(r)
-        return obs, r, bool(done[0].item()), self._info(info)
+        f64 = a.dtype == np.float64
+        b = self._b
+        if not hasattr(self, "_pk"):
+            n_o, n_u, d = self.n_o, self.n_u, b.device
+            self._pk = torch.zeros(n_o + 4, dtype=torch.float64, device=d)
+            self._pkh = torch.zeros(n_o + 4, dtype=torch.float64, pin_memory=True)
+            self._pkb = self._pkh.view(torch.uint8)
+            self._ah = {False: torch.zeros(n_u, dtype=torch.float32, pin_memory=True),
+                        True: torch.zeros(n_u, dtype=torch.float64, pin_memory=True)}
+            self._ad = {False: torch.zeros(n_u, dtype=torch.float32, device=d),
+                        True: torch.zeros(n_u, dtype=torch.float64, device=d)}
+        n_o = self.n_o
+        ah, ad = self._ah[f64], self._ad[f64]
+        ah.numpy()[:] = a.reshape(-1)
+        ad.copy_(ah, non_blocking=True)
+        base = self._pk.data_ptr()
+        at = (lambda k: ctypes.c_void_p(base + 8 * k))
+        rc = _lib.load().rcbf_env_step(ctypes.byref(b._prm_env), 1, _lib.ptr(b.x), _lib.ptr(b.aux),
+                                       _lib.ptr(b.step_count), _lib.ptr(b.episode), _lib.ptr(ad), int(f64),
+                                       at(0), _lib.ptr(b.obs), at(n_o), at(n_o + 1), at(n_o + 2), at(n_o + 3),
+                                       0, b._rng_seed(), b.env_offset, b._stream())
+        _lib.check(rc, "rcbf_env_step")
+        self._pkh.copy_(self._pk, non_blocking=True)
+        torch.cuda.current_stream(b.device).synchronize()
+        h = self._pkh.numpy()
+        obs = h[:n_o].copy()
+        r = np.float64(h[n_o]) if f64 else np.float32(h[n_o])
+        done = bool(self._pkb[8 * (n_o + 2)])
+        goal = bool(self._pkb[8 * (n_o + 3)])
+        return obs, r, done, self._info_host(float(h[n_o + 1]), goal)
 
     def render(self, mode="human", close=False):
         print("Ep_step = {}, \tState = {}".format(self.episode_step, self.state))
@@ -345,8 +374,8 @@ class SimulatedCarsEnv(_SingleEnv):
         o[1::2] /= 30.0
         return o
 
-    def _info(self, info):
-        return {"cost": float(info["cost"][0].item()), "goal_met": False}
+    def _info_host(self, cost, goal):
+        return {"cost": cost, "goal_met": False}
 
 
 class UnicycleEnv(_SingleEnv):
@@ -382,11 +411,10 @@ class UnicycleEnv(_SingleEnv):
     def goal_met(self):
         return np.linalg.norm(self.state[:2] - self.goal_pos) <= self.goal_size
 
-    def _info(self, info):
+    def _info_host(self, c, goal):
         out = {}
-        if bool(info["goal_met"][0].item()):
+        if goal:
             out["goal_met"] = True
-        c = float(info["cost"][0].item())
         if c > 0:
             out["cost"] = c
         return out

@@ -1,0 +1,68 @@
+"""Per-call host latency of the B = 1 drop-in surfaces the reference's
+training loop calls every env step (main.py:93-110): the gym env.step on a
+numpy action, CBFQPLayer.get_safe_action on 1-D device tensors, and
+RCBF_SAC.get_safe_action (rcbf_amd.sac_cbf) on one observation.  Prints one
+JSON line of microseconds per call (median of 5 runs of 200 calls)."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "sac-rcbf_amd")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def per_call_us(fn, n=200, reps=5):
+    for _ in range(20):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e6 / n)
+    return round(float(np.median(ts)), 1)
+
+
+def main():
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.envs import SimulatedCarsEnv, UnicycleEnv
+    from rcbf_amd.sac_cbf import get_safe_action
+
+    class A:
+        cuda = True
+
+    out = {}
+    rng = np.random.default_rng(0)
+    for name, env in (("cars", SimulatedCarsEnv()), ("unicycle", UnicycleEnv())):
+        n_u = env.action_space.shape[0]
+        acts = rng.uniform(-1, 1, (64, n_u)).astype(np.float32)
+        k = [0]
+
+        def step():
+            obs, r, done, info = env.step(acts[k[0] % 64])
+            k[0] += 1
+            if done:
+                env.reset()
+        out[f"{name}_env_step_us"] = per_call_us(step)
+        layer = CBFQPLayer(env, A(), gamma_b=20.0)
+        dm = DynamicsModel(env, A())
+        obs = env.reset()
+        st = torch.as_tensor(dm.get_state(obs), dtype=torch.float32, device="cuda")
+        mu, sg = dm.predict_disturbance(st)
+        u = torch.as_tensor(acts[0], device="cuda")
+        out[f"{name}_layer_safe_action_us"] = per_call_us(lambda: layer.get_safe_action(st, u, mu, sg))
+        ot = torch.as_tensor(obs, dtype=torch.float32, device="cuda")
+        out[f"{name}_sac_get_safe_action_us"] = per_call_us(lambda: get_safe_action(layer, ot, u, dm))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
