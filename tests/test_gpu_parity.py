@@ -337,12 +337,14 @@ def test_fused_safe_step_cars(solver):
     env.check_failures()
 
 
-@pytest.mark.parametrize("k", [3, 5])
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 8])
 def test_fused_safe_step_unicycle(k):
     from rcbf_amd.envs import BatchedUnicycleEnv
     B = 4096
     rng = np.random.default_rng(7 + k)
     hz = O.UNI["hazards"][:k]
+    if k > len(hz):  # up to RCBF_MAX_HAZARDS = 8: extra hazards at seeded positions
+        hz = np.concatenate([hz, rng.uniform(-2.5, 2.5, (k - len(hz), 2))])
     env = BatchedUnicycleEnv(B, hazards_locations=hz)
     x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
     ld = O.uni_goal_dist(x); st = np.zeros(B, np.int64)
