@@ -420,11 +420,17 @@ def next_rows(dev):
     tx = rng.normal(0, 1, (3000, 10))
     ty = 0.1 * np.sin(tx) + rng.normal(0, 0.05, (3000, 10))
     model = gp.GPDisturbanceModel(tx, ty, [(1.5, 0.2, 0.05)] * 10, device=dev)
-    for B in (256, 4096):
+    for B in (1, 256, 4096):
         x = torch.as_tensor(rng.normal(0, 1, (B, 10)), dtype=torch.float32, device=dev)
         ms = _time_graph(lambda: model.predict(x), 5, dev)
         out[f"gp_predict_N3000_B{B}"] = {"ms": round(ms, 4), "tflops": round(model.flops_per_query() * B / ms / 1e9, 1),
                                           "frac_fp32_mfma_157TF": round(model.flops_per_query() * B / ms / 1e9 / 157.3, 3)}
+    lr = gp.GPDisturbanceModel(tx, ty, [(1.5, 0.2, 0.05)] * 10, device=dev, rank=100)
+    for B in (1, 256, 4096):  # rank 100: the root-decomposition size of gpytorch's fast_pred_var
+        x = torch.as_tensor(rng.normal(0, 1, (B, 10)), dtype=torch.float32, device=dev)
+        ms = _time_graph(lambda: lr.predict(x), 5, dev)
+        out[f"gp_predict_N3000_rank100_B{B}"] = {"us": round(ms * 1e3, 2),
+                                                  "tflops": round(lr.flops_per_query() * B / ms / 1e9, 2)}
     B = 65536
     env = BatchedSimulatedCarsEnv(4, device=dev)
     prm = make_params(env, 1.0)

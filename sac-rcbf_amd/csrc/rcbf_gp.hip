@@ -36,9 +36,15 @@ constexpr int kGpChunk = 256;  // training rows staged in LDS at a time
 // current ones are consumed (register double buffer).
 // partial[(i * n_cb + cb) * B + b] = sum over this block's columns j < r of Q^2;
 // meanraw[i * B + b] = Q(b, r) from the block holding column r.
-template <int D, int CT>
+// Split-K (SK, small grids: few query tiles or a low-rank [R | alpha]):
+// blockIdx.z = i * n_split + s and the workgroup sums only training rows
+// [s per, (s + 1) per); it stores its raw Q tile to
+// qraw[((i * n_split + s) * B + b) * C_pad + col] and k_gp_combine adds the
+// n_split tiles (fixed order, deterministic) before squaring.
+template <int D, int CT, bool SK = false>
 __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
-                                                  float* __restrict__ partial, float* __restrict__ meanraw) {
+                                                  float* __restrict__ partial, float* __restrict__ meanraw,
+                                                  int n_split = 1, float* __restrict__ qraw = nullptr) {
     constexpr int DP = (D + 3) / 4 * 4;  // LDS row stride (float4 reads)
     constexpr float kL2E = 1.4426950408889634f;
     __shared__ float4 s_xt[kGpChunk * DP / 4];
@@ -46,7 +52,8 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
 
     // CT column tiles of 32 per wave: 4 (the whole 128-column block) or 2
     // (half of it, twice the workgroups for small query batches)
-    const int i = blockIdx.z;
+    const int i = SK ? (int)blockIdx.z / n_split : (int)blockIdx.z;
+    const int split = SK ? (int)blockIdx.z % n_split : 0;
     const int cb = blockIdx.y / (4 / CT);          // 128-column block
     const int sub = blockIdx.y % (4 / CT);         // which CT tiles of it
     const int n_part = gridDim.y;
@@ -86,8 +93,14 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
     // its B values for the 4 column tiles.
     const float* Rt_i = m.Rt + (int64_t)i * m.N_pad * ldc + (int64_t)cb * kGpCols + 4 * l32 + CT * sub;
 
-    for (int n0 = 0; n0 < m.N_pad; n0 += kGpChunk) {
-        const int nch = min(kGpChunk, m.N_pad - n0);  // multiple of 32
+    int n_beg = 0, n_end = m.N_pad;
+    if constexpr (SK) {
+        const int per = ((m.N_pad + n_split - 1) / n_split + 31) / 32 * 32;
+        n_beg = min(m.N_pad, split * per);
+        n_end = min(m.N_pad, n_beg + per);
+    }
+    for (int n0 = n_beg; n0 < n_end; n0 += kGpChunk) {
+        const int nch = min(kGpChunk, n_end - n0);  // multiple of 32
         __syncthreads();
         for (int e = threadIdx.x; e < nch; e += 256) {
             float v[DP];
@@ -146,6 +159,18 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
     }
 
     // epilogue: C layout col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    if constexpr (SK) {
+        float* qt = qraw + ((int64_t)i * n_split + split) * B * ldc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = b0 + 32 * w + (r & 3) + 8 * (r >> 2) + 4 * half;
+            if (row < B) {
+#pragma unroll
+                for (int c = 0; c < CT; ++c) qt[row * ldc + cb * kGpCols + 32 * (c + CT * sub) + l32] = acc[c][r];
+            }
+        }
+        return;
+    }
     const int r_rank = m.r;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -162,6 +187,33 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
         for (int msk = 1; msk < 32; msk <<= 1) v += __shfl_xor(v, msk, 64);
         if (l32 == 0 && row < B) partial[((int64_t)i * n_part + blockIdx.y) * B + row] = v;
     }
+}
+
+// Split-K combine: one wave per (GP i, column block cb, query b) adds the
+// n_split raw Q rows (fixed order) over the block's 128 columns, then
+// partial = sum_{col < r} Q^2 and meanraw = Q(b, r), as k_gp_qform's own epilogue.
+__global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, int n_cb, int n_split,
+                                                    const float* __restrict__ qraw, float* __restrict__ partial,
+                                                    float* __restrict__ meanraw) {
+    const int64_t wv = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wv >= (int64_t)m.n_s * n_cb * B) return;
+    const int64_t b = wv % B;
+    const int cb = (int)((wv / B) % n_cb);
+    const int i = (int)(wv / (B * n_cb));
+    const int64_t ldc = m.C_pad;
+    float v = 0.0f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int col = cb * kGpCols + 64 * h + lane;  // logical column: k_gp_qform stores Q by logical column
+        float q = 0.0f;
+        for (int s = 0; s < n_split; ++s) q += qraw[(((int64_t)i * n_split + s) * B + b) * ldc + col];
+        v += (col < m.r) ? q * q : 0.0f;
+        if (col == m.r) meanraw[(int64_t)i * B + b] = q;
+    }
+#pragma unroll
+    for (int msk = 1; msk < 64; msk <<= 1) v += __shfl_xor(v, msk, 64);
+    if (lane == 0) partial[((int64_t)i * n_cb + cb) * B + b] = v;
 }
 
 // mean/std (B, n_s) row-major like predict_disturbance's (n_test, n_s) output.
@@ -181,6 +233,24 @@ __global__ void __launch_bounds__(256) k_gp_finish(rcbf_gp_model m, int64_t B, i
     std_out[e] = sqrtf(var) * m.y_scale[i];
 }
 
+// Split-K factor: 1 when the (query tile x column block x GP) grid already
+// gives every CU several workgroups; otherwise enough splits of the training
+// rows for ~6 workgroups per CU (3 resident per CU at 160 VGPRs), each split
+// at least one 256-row LDS chunk.
+int gp_split(const rcbf_gp_model* m, int64_t B) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    const int64_t tiles = ((B + kGpRows - 1) / kGpRows) * (m->C_pad / kGpCols) * m->n_s;
+    const int64_t want = 6LL * cus;
+    if (tiles >= want / 2) return 1;
+    int64_t sk = (want + tiles - 1) / tiles;
+    const int64_t cap = m->N_pad / kGpChunk;
+    sk = sk < cap ? sk : cap;
+    return sk < 1 ? 1 : (int)sk;
+}
+
 }  // namespace
 
 extern "C" {
@@ -188,7 +258,9 @@ extern "C" {
 int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B) {
     if (!m || B < 0) return -1;
     const int64_t n_cb = m->C_pad / kGpCols;
-    return (int64_t)m->n_s * (2 * n_cb + 1) * B;  // partials for up to 2 launches per block, + means
+    const int sk = gp_split(m, B);
+    // partials for up to 2 launches per block, + means, + the split-K raw Q tiles
+    return (int64_t)m->n_s * (2 * n_cb + 1) * B + (sk > 1 ? (int64_t)sk * m->n_s * B * m->C_pad : 0);
 }
 
 int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out, float* std_out,
@@ -207,8 +279,18 @@ int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* me
     const int n_part = n_cb;
     float* partial = workspace;
     float* meanraw = workspace + (int64_t)m->n_s * 2 * n_cb * B;
-    dim3 g((unsigned)((B + kGpRows - 1) / kGpRows), (unsigned)n_part, (unsigned)m->n_s);
-#define RCBF_GP_L(DD) hipLaunchKernelGGL((k_gp_qform<DD, 4>), g, dim3(256), 0, stream, *m, B, x, partial, meanraw)
+    const int sk = gp_split(m, B);
+    float* qraw = meanraw + (int64_t)m->n_s * B;
+    dim3 g((unsigned)((B + kGpRows - 1) / kGpRows), (unsigned)n_part, (unsigned)(m->n_s * sk));
+#define RCBF_GP_L(DD)                                                                                           \
+    do {                                                                                                        \
+        if (sk > 1)                                                                                             \
+            hipLaunchKernelGGL((k_gp_qform<DD, 4, true>), g, dim3(256), 0, stream, *m, B, x, partial, meanraw, \
+                               sk, qraw);                                                                       \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_gp_qform<DD, 4>), g, dim3(256), 0, stream, *m, B, x, partial, meanraw, 1,    \
+                               nullptr);                                                                        \
+    } while (0)
     switch (m->n_s) {  // D = n_s: the GP inputs are the full state
         case 3:
             RCBF_GP_L(3);
@@ -220,6 +302,11 @@ int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* me
             return RCBF_E_BAD_SHAPE;
     }
 #undef RCBF_GP_L
+    if (sk > 1) {
+        const int64_t waves = (int64_t)m->n_s * n_cb * B;
+        hipLaunchKernelGGL(k_gp_combine, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, *m, B, n_cb, sk,
+                           qraw, partial, meanraw);
+    }
     const int64_t tot = B * m->n_s;
     hipLaunchKernelGGL(k_gp_finish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *m, B, n_part,
                        partial, meanraw, mean_out, std_out);

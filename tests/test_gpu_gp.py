@@ -106,3 +106,44 @@ def test_save_load_disturbance_models_round_trip(tmp_path):
     m1, s1 = dm2.predict_disturbance(q)
     assert torch.equal(m0, m1) and torch.equal(s0, s1)
     assert dm2.disturb_estimators.hyper == dm.disturb_estimators.hyper
+
+
+def test_gp_split_k_matches_single_pass():
+    """Small grids take the split-K path (training rows split over workgroups,
+    raw Q tiles summed in fixed order by k_gp_combine); a large batch of the
+    same queries takes the single-pass path.  Both meet the oracle bar."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(21)
+    tx, ty = _data(rng, 3000, 10)
+    hyper = [(rng.uniform(0.8, 2.5), rng.uniform(0.05, 0.5), rng.uniform(0.01, 0.2)) for _ in range(10)]
+    model = gp.GPDisturbanceModel(tx, ty, hyper)
+    qn = (rng.normal(0, 1, (8192, 10)) * tx.std(0)).astype(np.float32)
+    q = torch.as_tensor(qn, device="cuda")
+    m_big, s_big = model.predict(q)
+    mo, so = O.gp_predict(qn[:256], tx, ty, hyper)
+    # This random fit is ill-conditioned (small noise, N = 3000 in 10-D: large
+    # alternating alpha), and the single pass accumulates 1 500 MFMA k-steps in
+    # one fp32 accumulator: mean error 3.2e-4 max|mean| measured (r01aa), so its
+    # bar here is 1e-3.  Split-K sums shorter chains (3e-6 measured at B = 1).
+    m_bg, s_bg = m_big[:256].cpu().numpy(), s_big[:256].cpu().numpy()
+    assert np.max(np.abs(m_bg - mo)) <= 1e-3 * np.max(np.abs(mo))
+    assert np.max(np.abs(s_bg - so) / so) <= 1e-4
+    m_s, s_s = model.predict(q[:256].contiguous())
+    _check(m_s.cpu().numpy(), s_s.cpu().numpy(), mo, so)
+    m_1, s_1 = model.predict(q[:1].contiguous())  # B = 1: the most splits
+    assert np.max(np.abs(m_1.cpu().numpy() - mo[:1])) <= 2e-4 * np.max(np.abs(mo))
+    assert np.max(np.abs(s_1.cpu().numpy() - so[:1]) / so[:1]) <= 1e-4
+
+
+def test_gp_predict_low_rank_split_k():
+    """rank 100 (the root-decomposition size of gpytorch's fast_pred_var,
+    gp_model.py:97): one 128-column block per GP, so B = 256 runs split-K."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(8)
+    tx, ty = _data(rng, 1200, 3)
+    hyper = [(1.1, 0.25, 0.04), (1.6, 0.4, 0.08), (0.9, 0.2, 0.02)]
+    model = gp.GPDisturbanceModel(tx, ty, hyper, rank=100)
+    q = (rng.normal(0, 1, (256, 3)) * tx.std(0)).astype(np.float32)
+    mean, std = model.predict(torch.as_tensor(q, device="cuda"))
+    mo, so = O.gp_predict(q, tx, ty, hyper, rank=100)
+    _check(mean.cpu().numpy(), std.cpu().numpy(), mo, so)
