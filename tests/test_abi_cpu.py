@@ -55,6 +55,17 @@ def test_argument_validation_without_gpu():
     # empty batch is a no-op
     assert lib.rcbf_safe_action(ctypes.byref(p), 0, None, None, None, None, None, None, None, None) == 0
     assert lib.rcbf_qp_solve(ctypes.byref(p), 4, 4, 4, None, None, None, None, 1, None, None, None, None, None) == 1002
+    assert lib.rcbf_qp_solve_f64(ctypes.byref(p), 4, 2, 17, None, None, None, None, 1, None, None, None, None,
+                                 None) == 1002
+    assert lib.rcbf_qp_solve_f64(ctypes.byref(p), 4, 2, 4, None, None, None, None, 1, None, None, None, None,
+                                 None) == 1003
+    # rcbf_qp_backward: n in 1..3, m in 1..16, P/G/h/grad_z required, every gradient output optional
+    assert lib.rcbf_qp_backward(ctypes.byref(p), 4, 0, 4, None, None, None, None, 1, None, None, None, None, None,
+                                None) == 1002
+    assert lib.rcbf_qp_backward(ctypes.byref(p), 4, 3, 7, None, None, None, None, 1, None, None, None, None, None,
+                                None) == 1003
+    assert lib.rcbf_qp_backward(ctypes.byref(p), 0, 3, 7, None, None, None, None, 1, None, None, None, None, None,
+                                None) == 0
 
 
 def test_params_from_env_attributes():
