@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--solver", default="active_set", choices=["active_set", "pdipm"])
     ap.add_argument("--graph-steps", type=int, default=500,
                     help="fused steps per captured hipGraph (fewer replays: less host launch overhead in the wall time)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extra", action="store_true", help="also time the K-step rollout kernel and big batches")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (for PMC counter passes)")
@@ -91,7 +91,7 @@ def cpu_baseline(env_name, hazards, seconds):
             C.safe_step(env_name, x, aux, st, u, 20.0, hazards=hz, threads=threads)
             n += 1
             el = time.perf_counter() - t0
-            if el >= budget or n >= 10000:
+            if el >= budget or n >= 100000:
                 return n * B / el, n, el
 
     v1, n1, e1 = run(1, seconds * 0.3)

@@ -22,6 +22,7 @@ using namespace rcbf;
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kGpRows = 128;   // query rows per workgroup
 constexpr int kGpCols = 128;   // Rt columns per workgroup
@@ -189,6 +190,116 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
     }
 }
 
+// Few queries (B <= 8): the posterior is a GEMV per GP, bound by streaming
+// [R | alpha] (n_s N_pad C_pad fp32, 377 MB at the reference's N = 3000), so
+// it skips the MFMA tiles (127 of 128 query rows would be padding) and
+// streams Rt with one 16-B load per lane per training row.  Workgroup
+// (column chunk of 256, row split of 256, GP i): its 256 threads first build
+// k_i(x_b, x_n) of the split's rows for every query into LDS (the arithmetic
+// of k_gp_qform), then wave w accumulates rows 64w..64w+63, and the 4 waves
+// are summed through LDS.  The raw Q values go to qraw in the split-K layout
+// (row split = split index), combined by k_gp_combine.
+constexpr int kGvRows = 256;  // training rows per workgroup (64 per wave)
+constexpr int kGvCols = 256;  // physical Rt columns per workgroup (4 per lane)
+
+template <int D, int BQ>
+__global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
+                                                 int n_rs, float* __restrict__ qraw) {
+    constexpr float kL2E = 1.4426950408889634f;
+    __shared__ float s_k[BQ][kGvRows];
+    __shared__ float4 s_red[3][BQ][64];
+    const int cc = blockIdx.x, rs = blockIdx.y, i = blockIdx.z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const float sl = m.inv_sl[i];
+    const float log2s = __log2f(m.outscale[i]);
+    const int n0 = rs * kGvRows;
+    {
+        const int n = n0 + t;
+        const bool in = n < m.N_pad;
+        float xt[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) xt[k] = in ? m.xt[((int64_t)i * m.N_pad + n) * D + k] : 0.0f;
+        const float tn = in ? -kL2E * m.tn2[(int64_t)i * m.N_pad + n] : 0.0f;
+#pragma unroll
+        for (int b = 0; b < BQ; ++b) {
+            const int64_t row = b < B ? b : B - 1;
+            float nrm = 0.0f, xs2[D];
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const float xs = (float)((double)xq[row * D + k] / m.x_std[k]) * sl;
+                nrm = fmaf(xs, xs, nrm);
+                xs2[k] = 2.0f * kL2E * xs;
+            }
+            float arg = fmaf(-kL2E, nrm, log2s) + tn;
+#pragma unroll
+            for (int k = 0; k < D; ++k) arg = fmaf(xs2[k], xt[k], arg);
+            s_k[b][t] = in ? __builtin_amdgcn_exp2f(fminf(arg, log2s)) : 0.0f;
+        }
+    }
+    __syncthreads();
+    const int64_t ldc = m.C_pad;
+    const int pcol = cc * kGvCols + 4 * lane;  // physical column of this lane's first value
+    const bool colin = pcol < m.C_pad;
+    float4 acc[BQ];
+#pragma unroll
+    for (int b = 0; b < BQ; ++b) acc[b] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const int nr = min(64, m.N_pad - (n0 + 64 * w));  // rows of this wave (N_pad is a multiple of 32)
+    if (colin && nr > 0) {
+        const float* R = m.Rt + ((int64_t)i * m.N_pad + n0 + 64 * w) * ldc + pcol;
+        const float* kw = &s_k[0][64 * w];
+        if (nr == 64) {
+#pragma unroll 16
+            for (int r = 0; r < 64; ++r) {
+                const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(R + r * ldc));
+#pragma unroll
+                for (int b = 0; b < BQ; ++b) {
+                    const float kv = kw[b * kGvRows + r];
+                    acc[b].x = fmaf(kv, v.x, acc[b].x);
+                    acc[b].y = fmaf(kv, v.y, acc[b].y);
+                    acc[b].z = fmaf(kv, v.z, acc[b].z);
+                    acc[b].w = fmaf(kv, v.w, acc[b].w);
+                }
+            }
+        } else {
+            for (int r = 0; r < nr; ++r) {
+                const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(R + r * ldc));
+#pragma unroll
+                for (int b = 0; b < BQ; ++b) {
+                    const float kv = kw[b * kGvRows + r];
+                    acc[b].x = fmaf(kv, v.x, acc[b].x);
+                    acc[b].y = fmaf(kv, v.y, acc[b].y);
+                    acc[b].z = fmaf(kv, v.z, acc[b].z);
+                    acc[b].w = fmaf(kv, v.w, acc[b].w);
+                }
+            }
+        }
+    }
+    if (w > 0) {
+#pragma unroll
+        for (int b = 0; b < BQ; ++b) s_red[w - 1][b][lane] = acc[b];
+    }
+    __syncthreads();
+    if (w == 0 && colin) {
+        // physical column 4 l + c of a 128-column block holds logical column 32 c + l
+        const int blk = pcol / kGpCols, l = (pcol % kGpCols) / 4;
+#pragma unroll
+        for (int b = 0; b < BQ; ++b) {
+            if (b >= B) break;
+            float4 a = acc[b];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const float4 o = s_red[u][b][lane];
+                a.x += o.x, a.y += o.y, a.z += o.z, a.w += o.w;
+            }
+            float* dst = qraw + (((int64_t)i * n_rs + rs) * B + b) * ldc + blk * kGpCols + l;
+            dst[0] = a.x;
+            dst[32] = a.y;
+            dst[64] = a.z;
+            dst[96] = a.w;
+        }
+    }
+}
+
 // Split-K combine: one wave per (GP i, column block cb, query b) adds the
 // n_split raw Q rows (fixed order) over the block's 128 columns, then
 // partial = sum_{col < r} Q^2 and meanraw = Q(b, r), as k_gp_qform's own epilogue.
@@ -237,7 +348,10 @@ __global__ void __launch_bounds__(256) k_gp_finish(rcbf_gp_model m, int64_t B, i
 // gives every CU several workgroups; otherwise enough splits of the training
 // rows for ~6 workgroups per CU (3 resident per CU at 160 VGPRs), each split
 // at least one 256-row LDS chunk.
+constexpr int kGvMaxB = 8;  // B <= 8: the streaming GEMV path
+
 int gp_split(const rcbf_gp_model* m, int64_t B) {
+    if (B <= kGvMaxB) return (m->N_pad + kGvRows - 1) / kGvRows;  // GEMV row splits
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
@@ -260,7 +374,8 @@ int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B) {
     const int64_t n_cb = m->C_pad / kGpCols;
     const int sk = gp_split(m, B);
     // partials for up to 2 launches per block, + means, + the split-K raw Q tiles
-    return (int64_t)m->n_s * (2 * n_cb + 1) * B + (sk > 1 ? (int64_t)sk * m->n_s * B * m->C_pad : 0);
+    const bool raw = sk > 1 || B <= kGvMaxB;
+    return (int64_t)m->n_s * (2 * n_cb + 1) * B + (raw ? (int64_t)sk * m->n_s * B * m->C_pad : 0);
 }
 
 int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out, float* std_out,
@@ -281,7 +396,34 @@ int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* me
     float* meanraw = workspace + (int64_t)m->n_s * 2 * n_cb * B;
     const int sk = gp_split(m, B);
     float* qraw = meanraw + (int64_t)m->n_s * B;
-    dim3 g((unsigned)((B + kGpRows - 1) / kGpRows), (unsigned)n_part, (unsigned)(m->n_s * sk));
+    if (B <= kGvMaxB) {
+        dim3 gv((unsigned)((m->C_pad + kGvCols - 1) / kGvCols), (unsigned)sk, (unsigned)m->n_s);
+#define RCBF_GV_L(DD, BB) hipLaunchKernelGGL((k_gp_gemv<DD, BB>), gv, dim3(256), 0, stream, *m, B, x, sk, qraw)
+#define RCBF_GV_B(DD)           \
+    do {                        \
+        if (B == 1)             \
+            RCBF_GV_L(DD, 1);   \
+        else if (B == 2)        \
+            RCBF_GV_L(DD, 2);   \
+        else if (B <= 4)        \
+            RCBF_GV_L(DD, 4);   \
+        else                    \
+            RCBF_GV_L(DD, 8);   \
+    } while (0)
+        switch (m->n_s) {
+            case 3:
+                RCBF_GV_B(3);
+                break;
+            case 10:
+                RCBF_GV_B(10);
+                break;
+            default:
+                return RCBF_E_BAD_SHAPE;
+        }
+#undef RCBF_GV_B
+#undef RCBF_GV_L
+    } else {
+        dim3 g((unsigned)((B + kGpRows - 1) / kGpRows), (unsigned)n_part, (unsigned)(m->n_s * sk));
 #define RCBF_GP_L(DD)                                                                                           \
     do {                                                                                                        \
         if (sk > 1)                                                                                             \
@@ -291,18 +433,19 @@ int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* me
             hipLaunchKernelGGL((k_gp_qform<DD, 4>), g, dim3(256), 0, stream, *m, B, x, partial, meanraw, 1,    \
                                nullptr);                                                                        \
     } while (0)
-    switch (m->n_s) {  // D = n_s: the GP inputs are the full state
-        case 3:
-            RCBF_GP_L(3);
-            break;
-        case 10:
-            RCBF_GP_L(10);
-            break;
-        default:
-            return RCBF_E_BAD_SHAPE;
-    }
+        switch (m->n_s) {  // D = n_s: the GP inputs are the full state
+            case 3:
+                RCBF_GP_L(3);
+                break;
+            case 10:
+                RCBF_GP_L(10);
+                break;
+            default:
+                return RCBF_E_BAD_SHAPE;
+        }
 #undef RCBF_GP_L
-    if (sk > 1) {
+    }
+    if (sk > 1 || B <= kGvMaxB) {
         const int64_t waves = (int64_t)m->n_s * n_cb * B;
         hipLaunchKernelGGL(k_gp_combine, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, *m, B, n_cb, sk,
                            qraw, partial, meanraw);

@@ -26,7 +26,7 @@ hyper = [(1.5, 0.2, 0.05)] * n_s
 model = gp.GPDisturbanceModel(tx, ty, hyper, rank=rank)
 PEAK = 157.3  # TFLOP/s dense fp32 MFMA (MI355X_MICROARCH.md)
 out = {"n_s": n_s, "N": N, "rank": model.r, "C_pad": model._m.C_pad}
-for B in (256, 4096, 65536):
+for B in (1, 8, 256, 4096, 65536):
     x = torch.as_tensor(rng.normal(0, 1, (B, n_s)), dtype=torch.float32, device="cuda")
     for _ in range(2):
         model.predict(x)
@@ -41,5 +41,6 @@ for B in (256, 4096, 65536):
     ms = e0.elapsed_time(e1) / reps
     fl = model.flops_per_query() * B
     out[f"B{B}"] = {"ms": round(ms, 4), "queries_per_s": round(B / (ms * 1e-3), 1),
-                    "tflops": round(fl / (ms * 1e-3) / 1e12, 2), "frac_fp32_mfma": round(fl / (ms * 1e-3) / 1e12 / PEAK, 4)}
+                    "tflops": round(fl / (ms * 1e-3) / 1e12, 2), "frac_fp32_mfma": round(fl / (ms * 1e-3) / 1e12 / PEAK, 4),
+                    "Rt_stream_GBs": round(model.Rt.numel() * 4 / (ms * 1e-3) / 1e9, 1)}  # HBM-bound at B <= 8
 print(json.dumps(out))

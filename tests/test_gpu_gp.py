@@ -27,7 +27,8 @@ def _check(m, s, mo, so):
     assert np.max(np.abs(s - so) / so) <= 1e-4
 
 
-@pytest.mark.parametrize("n_s,N,B", [(3, 300, 1), (3, 1100, 4096), (10, 1000, 200), (10, 3000, 257)])
+@pytest.mark.parametrize("n_s,N,B", [(3, 300, 1), (3, 1100, 4096), (10, 1000, 200), (10, 3000, 257),
+                                     (10, 3000, 1), (10, 1000, 5), (3, 300, 8), (3, 1100, 2)])
 def test_gp_predict_vs_oracle(n_s, N, B):
     from rcbf_amd import gp
     rng = np.random.default_rng(n_s * N + B)
