@@ -1,6 +1,6 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
-OUT=gpurun_out/r01ad; mkdir -p $OUT
+OUT=gpurun_out/r01ae; mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_gpu_gp.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 for lib in base main; do
