@@ -352,7 +352,11 @@ __device__ __forceinline__ void state_from_obs32(const float* o, float* s32) {
     } else {
         s32[0] = o[0];
         s32[1] = o[1];
+#ifdef RCBF_STUDY_NO_ATAN2  // performance study only: what the atan2 costs (wrong state)
+        s32[2] = o[3] + o[2];
+#else
         s32[2] = (float)atan2((double)o[3], (double)o[2]);
+#endif
     }
 }
 

@@ -1377,7 +1377,12 @@ __device__ __forceinline__ void uni_rows_diff(const rcbf_params& prm, const floa
     const float lp = (float)prm.l_p, g = (float)prm.gamma_b;
     // fp32 cos/sin, correctly rounded from fp64 (torch's SLEEF is within 1 ulp)
     double sd, cd;
+#ifdef RCBF_STUDY_NO_ROW_SINCOS  // performance study only: what the row sincos costs (wrong rows)
+    sd = (double)xs[2];
+    cd = 1.0 - 0.5 * sd * sd;
+#else
     sincos((double)xs[2], &sd, &cd);  // one shared range reduction
+#endif
     float c = (float)cd;
     float s = (float)sd;
     float px = xs[0] + lp * c, py = xs[1] + lp * s;
