@@ -101,6 +101,39 @@ def cpu_baseline(env_name, hazards, seconds):
                       f"{eN:.1f} s on {threads_all} threads; 1 thread: {v1:.4g} steps/s ({n1} steps)"}
 
 
+def cpu_reference_mode(env_name, hazards, seconds):
+    """The reference's own CPU mode restated (oracle/torch_mirror.py): fp32
+    rows, normaliser, qpth-style batched PDIPM in torch fp64 (eps 1e-4,
+    notImprovedLim 10, capped at 100 iterations), clamp, numpy env step, on
+    the same 65536 envs, on the torch threads of this host."""
+    from oracle import oracle as O
+    from oracle import torch_mirror as M
+    B = 65536
+    rng = np.random.default_rng(1)
+    threads = torch.get_num_threads()
+    if env_name == "SimulatedCars":
+        x, aux, st = O.cars_reset(rng.normal(0, 0.5, B))
+    else:
+        hz = O.UNI["hazards"][:hazards]
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        aux, st = O.uni_goal_dist(x), np.zeros(B, np.int64)
+    n_u = 1 if env_name == "SimulatedCars" else 2
+    n, its, t0 = 0, 0, time.perf_counter()
+    while True:
+        u = rng.uniform(-1, 1, (B, n_u)).astype(np.float32)
+        if env_name == "SimulatedCars":
+            x, aux, st, _, k = M.cars_safe_step(x, aux, st, u, 20.0)
+        else:
+            x, aux, st, _, k = M.uni_safe_step(x, aux, st, u, 20.0, hz)
+        n, its = n + 1, its + k
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(n * B / el, 1), "unit": "safe env steps/s", "cores": threads, "kind": "port",
+            "sample": f"reference CPU mode restated (oracle/torch_mirror.py: torch-CPU qpth-style PDIPM, "
+                      f"{its / n:.1f} iterations per step), {n} steps x {B} envs in {el:.1f} s on {threads} threads"}
+
+
 def pmc_traffic(env_name, B):
     """HBM bytes per launch of k_safe_step from the committed rocprofv3 PMC
     passes (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, gfx950
@@ -263,6 +296,7 @@ def main():
         rec["extra"] = extra
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(args.env, args.hazards, args.cpu_seconds)
+        rec["cpu_reference_mode"] = cpu_reference_mode(args.env, args.hazards, args.cpu_seconds / 3)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
