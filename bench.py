@@ -130,7 +130,7 @@ def cpu_reference_mode(env_name, hazards, seconds):
         if el >= seconds:
             break
     return {"value": round(n * B / el, 1), "unit": "safe env steps/s", "cores": threads, "kind": "port",
-            "sample": f"reference CPU mode restated (oracle/torch_mirror.py: torch-CPU qpth-style PDIPM, "
+            "sample": f"reference CPU mode restated (oracle/torch_mirror.py: torch-CPU qpth-style PDIPM, from seeded resets, "
                       f"{its / n:.1f} iterations per step), {n} steps x {B} envs in {el:.1f} s on {threads} threads"}
 
 
