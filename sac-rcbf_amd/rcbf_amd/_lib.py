@@ -135,7 +135,12 @@ def ptr(t):
 
 
 def stream_of(device):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """torch's current HIP stream on `device` (raw handle, without building a
+    torch.cuda.Stream object: ~0.3 us instead of ~2.4 us per call)."""
+    idx = device.index if isinstance(device, torch.device) else device
+    if idx is None:
+        idx = torch.cuda.current_device()
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(idx))
 
 
 def require_device(t, name):

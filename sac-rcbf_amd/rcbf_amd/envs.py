@@ -120,6 +120,8 @@ class BatchedEnv:
         if not torch.cuda.is_available():
             raise RuntimeError("device envs need a HIP device (MI355X); there is no CPU fallback")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.num_envs = int(num_envs)
         self.seed_value = int(seed)
         self.env_offset = int(env_offset)  # global index of env 0 (sharding)
@@ -208,17 +210,29 @@ class BatchedEnv:
         CBFQPLayer.get_safe_action(state, u_rl, mean, sigma) -> env.step.
         mean/sigma None -> the DynamicsModel prior in-kernel.  `outputs`
         (from make_outputs) avoids per-call allocation; failures accumulate
-        in self.fail_flag (check with check_failures())."""
+        in self.fail_flag (check with check_failures()).
+        The ctypes argument list is cached per (layer, outputs tensors,
+        auto_reset): an eager call then costs one data_ptr per changing
+        input, so the host keeps pace with the ~4 us kernel."""
         B, d = self.num_envs, self.device
         o = outputs if outputs is not None else self.make_outputs()
         u = u_rl if (torch.is_tensor(u_rl) and u_rl.dtype == torch.float32 and u_rl.is_contiguous()
                      and u_rl.device == d) else torch.as_tensor(u_rl, dtype=torch.float32, device=d).contiguous()
-        rc = _lib.load().rcbf_safe_step(ctypes.byref(layer._prm), B, _lib.ptr(self.x), _lib.ptr(self.aux),
-                                        _lib.ptr(self.step_count), _lib.ptr(self.episode), _lib.ptr(u),
-                                        _lib.ptr(mean), _lib.ptr(sigma), _lib.ptr(self.obs), _lib.ptr(o["u"]),
-                                        _lib.ptr(o["reward"]), _lib.ptr(o["cost"]), _lib.ptr(o["done"]),
-                                        _lib.ptr(o["goal_met"]), None, _lib.ptr(self.fail_flag), int(auto_reset),
-                                        self._rng_seed(), self.env_offset, self._stream())
+        key = (id(layer), auto_reset, tuple(map(id, o.values())))
+        ent = self._ss_cache.get(key) if hasattr(self, "_ss_cache") else None
+        if ent is None or ent[0] is not layer or ent[1] is not o:
+            self._ss_cache = {}
+            args = [ctypes.byref(layer._prm), B, _lib.ptr(self.x), _lib.ptr(self.aux), _lib.ptr(self.step_count),
+                    _lib.ptr(self.episode), None, None, None, _lib.ptr(self.obs), _lib.ptr(o["u"]),
+                    _lib.ptr(o["reward"]), _lib.ptr(o["cost"]), _lib.ptr(o["done"]), _lib.ptr(o.get("goal_met")),
+                    None, _lib.ptr(self.fail_flag), int(auto_reset), self._rng_seed(), self.env_offset, None]
+            ent = self._ss_cache[key] = (layer, o, args, [t for t in o.values() if t is not None])
+        args = ent[2]
+        args[6] = u.data_ptr()
+        args[7] = None if mean is None else mean.data_ptr()
+        args[8] = None if sigma is None else sigma.data_ptr()
+        args[20] = torch._C._cuda_getCurrentRawStream(d.index)
+        rc = _lib.load().rcbf_safe_step(*args)
         _lib.check(rc, "rcbf_safe_step")
         return self.obs, o["reward"], o["done"], o
 
