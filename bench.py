@@ -282,7 +282,8 @@ def main():
         "data": "synthetic (SURVEY 8(d) start states, u_RL ~ U[-1,1], prior mean/sigma, seeded auto-resets)",
         "config": {"workload": f"{args.env} fused safe step (rcbf_safe_step), non-diff CBF-QP, "
                                f"{'3-hazard ' if args.env == 'Unicycle' and args.hazards == 3 else ''}"
-                               f"batch {B} envs per GPU, {args.solver} fp64 QP, hipGraph of {S} steps",
+                               f"batch {B} envs per GPU, {args.solver} fp64 QP, "
+                               f"{'eager launches' if args.no_graph else f'hipGraph of {S} steps'}",
                    "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
                    "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)",
                    "qp_active_frac_at_start": round(active_frac, 4)},

@@ -25,6 +25,11 @@ import torch
 from . import _lib
 from .params import make_params
 
+try:  # optional CPython binding of rcbf_safe_step (built next to librcbf_hip.so by build())
+    from . import _rcbf_fast as _fast
+except ImportError:
+    _fast = None
+
 try:  # keep gym's types when gym is installed (it is not in this image)
     import gym as _gym
     _EnvBase = _gym.Env
@@ -222,17 +227,23 @@ class BatchedEnv:
         ent = self._ss_cache.get(key) if hasattr(self, "_ss_cache") else None
         if ent is None or ent[0] is not layer or ent[1] is not o:
             self._ss_cache = {}
-            args = [ctypes.byref(layer._prm), B, _lib.ptr(self.x), _lib.ptr(self.aux), _lib.ptr(self.step_count),
-                    _lib.ptr(self.episode), None, None, None, _lib.ptr(self.obs), _lib.ptr(o["u"]),
-                    _lib.ptr(o["reward"]), _lib.ptr(o["cost"]), _lib.ptr(o["done"]), _lib.ptr(o.get("goal_met")),
-                    None, _lib.ptr(self.fail_flag), int(auto_reset), self._rng_seed(), self.env_offset, None]
+
+            def p(t):
+                return 0 if t is None else t.data_ptr()
+            args = [ctypes.addressof(layer._prm), B, p(self.x), p(self.aux), p(self.step_count), p(self.episode),
+                    0, 0, 0, p(self.obs), p(o["u"]), p(o["reward"]), p(o["cost"]), p(o["done"]),
+                    p(o.get("goal_met")), 0, p(self.fail_flag), int(auto_reset), self._rng_seed(), self.env_offset, 0]
             ent = self._ss_cache[key] = (layer, o, args, [t for t in o.values() if t is not None])
         args = ent[2]
         args[6] = u.data_ptr()
-        args[7] = None if mean is None else mean.data_ptr()
-        args[8] = None if sigma is None else sigma.data_ptr()
+        args[7] = 0 if mean is None else mean.data_ptr()
+        args[8] = 0 if sigma is None else sigma.data_ptr()
         args[20] = torch._C._cuda_getCurrentRawStream(d.index)
-        rc = _lib.load().rcbf_safe_step(*args)
+        if _fast is not None:  # CPython binding (csrc/rcbf_pyfast.cpp): ~1 us instead of ~4 us through ctypes
+            rc = _fast.safe_step(*args)
+        else:
+            rc = _lib.load().rcbf_safe_step(ctypes.byref(layer._prm), B, *[a or None for a in args[2:17]],
+                                            *args[17:20], args[20] or None)
         _lib.check(rc, "rcbf_safe_step")
         return self.obs, o["reward"], o["done"], o
 

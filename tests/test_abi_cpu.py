@@ -138,3 +138,19 @@ def test_cascade_get_cbfs_and_min_h():
     assert cl.get_min_h_val(s) == np.min(get_h(s))
     centre = np.array([hz[0, 0] - 0.03, hz[0, 1], 0.0])
     assert abs(cl.get_min_h_val(centre) + 0.5 * 0.67 ** 2) < 1e-12
+
+
+def test_fast_binding_loads_and_validates():
+    """The CPython binding of rcbf_safe_step (csrc/rcbf_pyfast.cpp) is built
+    next to librcbf_hip.so and forwards to the same C-ABI (argument checks run
+    before any launch, so this needs no GPU)."""
+    from rcbf_amd import _lib, _rcbf_fast
+    p = _lib.RcbfParams()
+    p.mode = _lib.MODE_SIMULATED_CARS
+    a = ctypes.addressof(p)
+    assert _rcbf_fast.safe_step(a, 0, *([0] * 19)) == 0          # empty batch: no-op
+    assert _rcbf_fast.safe_step(a, 4, *([0] * 19)) == 1003       # NULL buffers
+    p.mode = 9
+    assert _rcbf_fast.safe_step(a, 4, *([0] * 19)) == 1001       # bad mode
+    with pytest.raises(TypeError):
+        _rcbf_fast.safe_step(a, 4)
