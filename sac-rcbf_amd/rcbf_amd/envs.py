@@ -210,6 +210,18 @@ class BatchedEnv:
             info["obs64"] = o64
         return self.obs, reward, done.bool(), info
 
+    def _prior_arg(self, t, name):
+        """mean / sigma as the kernel reads them: (B, n_s) fp32, contiguous, on
+        this env's device (None -> the in-kernel prior)."""
+        if t is None:
+            return None
+        B, d = self.num_envs, self.device
+        if not (torch.is_tensor(t) and t.dtype == torch.float32 and t.is_contiguous() and t.device == d):
+            t = torch.as_tensor(t, dtype=torch.float32, device=d).contiguous()
+        if t.shape != (B, self.n_s):
+            raise ValueError(f"{name} must be ({B}, {self.n_s}), got {tuple(t.shape)}")
+        return t
+
     def safe_step(self, u_rl, layer, mean=None, sigma=None, auto_reset=True, outputs=None):
         """The fused hot path (rcbf_safe_step): state -> get_state(obs32) ->
         CBFQPLayer.get_safe_action(state, u_rl, mean, sigma) -> env.step.
@@ -223,7 +235,10 @@ class BatchedEnv:
         o = outputs if outputs is not None else self.make_outputs()
         u = u_rl if (torch.is_tensor(u_rl) and u_rl.dtype == torch.float32 and u_rl.is_contiguous()
                      and u_rl.device == d) else torch.as_tensor(u_rl, dtype=torch.float32, device=d).contiguous()
-        key = (id(layer), auto_reset, tuple(map(id, o.values())))
+        if u.shape != (B, self.n_u):
+            raise ValueError(f"u_rl must be ({B}, {self.n_u}), got {tuple(u.shape)}")
+        mean, sigma = self._prior_arg(mean, "mean"), self._prior_arg(sigma, "sigma")
+        key =(id(layer), auto_reset, tuple(map(id, o.values())))
         ent = self._ss_cache.get(key) if hasattr(self, "_ss_cache") else None
         if ent is None or ent[0] is not layer or ent[1] is not o:
             self._ss_cache = {}

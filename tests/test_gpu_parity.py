@@ -408,6 +408,54 @@ def test_fused_step_ragged_batches_match_full_batch(mode):
     assert int(full.episode.max().item()) >= 2  # auto-resets happened (construction counts as episode 1)
 
 
+@pytest.mark.parametrize("mode", ["SimulatedCars", "Unicycle"])
+def test_fast_binding_matches_ctypes_path(mode, monkeypatch):
+    """safe_step through the CPython binding (csrc/rcbf_pyfast.cpp) and through
+    ctypes launch the same C-ABI entry point: bit-identical trajectories, with
+    and without a disturbance prior, auto-resets included, on a side stream."""
+    import rcbf_amd.envs as E
+    assert E._fast is not None, "_rcbf_fast extension not built (run __graft_entry__.build())"
+    B = 1000
+    rng = np.random.default_rng(5)
+    us = [dev(rng.uniform(-1, 1, (B, 1 if mode == "SimulatedCars" else 2))) for _ in range(12)]
+
+    def run(fast):
+        monkeypatch.setattr(E, "_fast", fast)
+        if mode == "SimulatedCars":
+            e = E.BatchedSimulatedCarsEnv(B, seed=8)
+        else:
+            e = E.BatchedUnicycleEnv(B, seed=8, hazards_locations=O.UNI["hazards"][:3])
+        lay = _layer(e, 20.0)
+        mu = torch.full((B, e.n_s), 0.01, device="cuda")
+        sg = torch.full((B, e.n_s), 0.2, device="cuda")
+        got = []
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for k, u in enumerate(us):
+                obs, r, d, out = e.safe_step(u, lay, mean=mu if k % 2 else None, sigma=sg if k % 2 else None)
+                got += [obs.clone(), r.clone(), d.clone(), out["u"].clone()]
+        torch.cuda.synchronize()
+        e.check_failures()
+        return got + [e.state.clone(), e.step_count.clone()]
+
+    fast = E._fast
+    a, b = run(fast), run(None)
+    for g, w in zip(a, b):
+        assert torch.equal(g, w)
+    # malformed inputs are refused on the host, before any launch
+    monkeypatch.setattr(E, "_fast", fast)
+    e = E.BatchedSimulatedCarsEnv(8, seed=1)
+    lay = _layer(e, 20.0)
+    u = torch.zeros(8, 1, device="cuda")
+    with pytest.raises(ValueError):
+        e.safe_step(u, lay, mean=torch.zeros(8, 3, device="cuda"))
+    with pytest.raises(ValueError):
+        e.safe_step(torch.zeros(4, 1, device="cuda"), lay)
+    e.safe_step(u, lay, mean=torch.zeros(8, 10, dtype=torch.float64, device="cuda"))  # converted to fp32
+    e.check_failures()
+
+
 def test_rollout_matches_single_steps():
     """K fused steps in one launch == K launches of the fused step."""
     from rcbf_amd.envs import BatchedSimulatedCarsEnv
