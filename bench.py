@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extra", action="store_true", help="also time the K-step rollout kernel and big batches")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (for PMC counter passes)")
+    ap.add_argument("--launch", default="graph", choices=["graph", "seq"],
+                    help="graph: hipGraph replays of --graph-steps fused steps; seq: the K launches issued from "
+                         "one host call (rcbf_safe_step_seq)")
     return ap.parse_args()
 
 
@@ -205,7 +208,7 @@ def main():
         env = BatchedUnicycleEnv(B, device=dev, seed=1234, env_offset=shard.env_offset(rank, B),
                                  hazards_locations=UNI["hazards"][:args.hazards])
     layer = CBFQPLayer(env, LArgs(), gamma_b=20.0, solver=solver)
-    S = largest_divisor_le(args.steps, args.graph_steps)
+    S = args.steps if args.launch == "seq" else largest_divisor_le(args.steps, args.graph_steps)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
     init_states(env, gen, args.env)
@@ -225,7 +228,13 @@ def main():
     # warmup (eager), then capture S fused steps into one hipGraph
     steps(max(args.warmup, 1))
     torch.cuda.synchronize()
-    if args.no_graph:
+    if args.launch == "seq" and not args.no_graph:
+        class _Seq:
+            def replay(self):
+                env.safe_step_seq(pool, layer, outputs=outs, steps=S)
+        graph = _Seq()
+        graph.replay()
+    elif args.no_graph:
         class _Eager:
             def replay(self):
                 steps(S)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 4
+#define RCBF_ABI_VERSION 5
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -269,6 +269,24 @@ int rcbf_env_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int
                   float* obs_out, double* reward, double* cost, uint8_t* done, uint8_t* goal_met,
                   int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream);
 
+/* The reference's per-step gym call (env.step at main.py:95) for a small
+ * batch that lives on the device but talks to the host: the action is READ
+ * from host memory and obs64 / reward / cost / done / goal_met are WRITTEN
+ * to host memory by the kernel itself (zero copy, both buffers from
+ * rcbf_host_alloc), then the call waits for the stream.  One host call, no
+ * copy launches.  packed_host (8 B (n_o + 2) + 2 B bytes) holds
+ *   obs64 (B, n_o) f64 | reward (B,) f64 | cost (B,) f64 | done (B,) u8 | goal_met (B,) u8.
+ * action_host (B, n_u) f32 (action_f64 = 0) or f64 (action_f64 = 1).
+ * Same arithmetic as rcbf_env_step. */
+int rcbf_env_step_sync(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step,
+                       uint32_t* episode, const void* action_host, int32_t action_f64, double* packed_host,
+                       int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream);
+
+/* Pinned, device-coherent host memory for rcbf_env_step_sync (set-up only,
+ * never on the per-step path).  Returns hipError_t; *ptr = NULL on failure. */
+int rcbf_host_alloc(int64_t bytes, void** ptr);
+int rcbf_host_free(void* ptr);
+
 /* The fused safe step -- the hot path measured by bench.py:
  *   obs32 = float(obs(x)); state = get_state(obs32) (dynamics.py:190-232);
  *   mean,sigma = prior or given; u = CBFQPLayer.get_safe_action(state, u_rl,
@@ -281,6 +299,21 @@ int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, in
                    float* obs_out, float* u_out, float* reward, float* cost, uint8_t* done,
                    uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag,
                    int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream);
+
+/* K fused safe steps issued back to back from one host call: K launches of
+ * the same kernel as rcbf_safe_step on `stream` (each step reads and writes
+ * the env state in HBM; outputs are overwritten each step).  Step j reads the
+ * policy actions u_rl_seq[j % n_u_rl], a HOST array of n_u_rl device
+ * pointers, each (B, n_u) f32.  The batched training / warm-up loop
+ * (main.py:47-110 with actions already on the device) without a Python
+ * round trip or a graph launch per step.  Stops at the first failing launch
+ * and returns its error. */
+int rcbf_safe_step_seq(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux,
+                       int32_t* step, uint32_t* episode, const float* const* u_rl_seq, int32_t n_u_rl,
+                       const float* mu, const float* sigma, float* obs_out, float* u_out, float* reward,
+                       float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
+                       int32_t* fail_flag, int32_t auto_reset, uint64_t seed, int64_t env_offset,
+                       hipStream_t stream);
 
 /* K fused safe steps in ONE launch with the env state held in registers
  * (a pre-sampled u_rl (K, B, n_u), e.g. the reference's warm-up phase that

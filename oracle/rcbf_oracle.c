@@ -314,11 +314,32 @@ int oracle_safe_action(int mode, int K, const double* hz, double gamma_b, int64_
     return fails;
 }
 
-/* The fused safe step (the hot path bench.py measures), prior mean/sigma,
- * no auto-reset: state -> get_state(obs32) -> safe action -> env.step. */
-int oracle_safe_step(int mode, int K, const double* hz, double gamma_b, int64_t B, double* x, double* aux,
-                     int32_t* step, const float* u, float* u_out, float* rew, float* cost, uint8_t* done,
-                     int nthreads) {
+/* observations as the policy sees them (fp32): simulated_cars_env.py:143-158,
+ * unicycle_env.py:215-231 + obs_compass :260-277 */
+static void cars_obs32(const double* xs, float* o) {
+    for (int k = 0; k < 10; ++k) o[k] = (float)(xs[k] / ((k & 1) ? 30.0 : 100.0));
+}
+
+static void uni_obs32(const double* xs, float* o) {
+    double r0 = 2.5 - xs[0], r1 = 2.5 - xs[1];
+    double gd = sqrt(r0 * r0 + r1 * r1), c = cos(xs[2]), s = sin(xs[2]);
+    double v0 = r0 * c + r1 * s, v1 = r0 * (-s) + r1 * c;
+    double nrm = sqrt(v0 * v0 + v1 * v1) + 0.001;
+    o[0] = (float)xs[0]; o[1] = (float)xs[1]; o[2] = (float)c; o[3] = (float)s;
+    o[4] = (float)(v0 / nrm); o[5] = (float)(v1 / nrm); o[6] = (float)exp(-gd);
+}
+
+/* The fused safe step (the hot path bench.py measures): state ->
+ * get_state(obs32) -> CBFQPLayer.get_safe_action (mean/sigma NULL -> the
+ * DynamicsModel prior, dynamics.py:381-384) -> env.step -> obs; with
+ * auto_reset a finished env is reset (simulated_cars_env.py:108-125 /
+ * unicycle_env.py:125-143) and its obs is that of the reset state.  The cars
+ * reset velocity draw is injected (reset_noise[i] = the N(0, 0.5) sample,
+ * NULL -> 0).  obs_out / goal_out may be NULL. */
+int oracle_safe_step_ex(int mode, int K, const double* hz, double gamma_b, int64_t B, double* x, double* aux,
+                        int32_t* step, const float* u, const float* mu_in, const float* sig_in, float* u_out,
+                        float* rew, float* cost, uint8_t* done, uint8_t* goal_out, float* obs_out, int auto_reset,
+                        const double* reset_noise, int nthreads) {
     int fails = 0;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -333,7 +354,7 @@ int oracle_safe_step(int mode, int K, const double* hz, double gamma_b, int64_t 
                 double sc = (k & 1) ? 30.0 : 100.0;
                 float o = (float)(xs[k] / sc);
                 s32[k] = (float)((double)o * sc);
-                sig[k] = (k & 1) ? (float)0.2 : 0.0f;
+                sig[k] = sig_in ? sig_in[i * 10 + k] : ((k & 1) ? (float)0.2 : 0.0f);
             }
             cars_rows(s32, u[i], sig, gamma_b, G, h);
             normalize(4, 2, G, h);
@@ -343,13 +364,26 @@ int oracle_safe_step(int mode, int K, const double* hz, double gamma_b, int64_t 
             float a = fminf(fmaxf(v, -10.0f), 10.0f);
             u_out[i] = a;
             cars_env(xs, aux + i, step + i, a, rew + i, cost + i, done + i);
+            if (goal_out) goal_out[i] = 0;
+            if (auto_reset && done[i]) {
+                const double nz = reset_noise ? reset_noise[i] : 0.0;
+                const double p0[5] = {34.0, 28.0, 22.0, 16.0, 10.0};
+                for (int c = 0; c < 5; ++c) { xs[2 * c] = p0[c]; xs[2 * c + 1] = 30.0 + nz; }
+                xs[7] = 35.0;
+                aux[i] = 0.0;
+                step[i] = 0;
+            }
+            if (obs_out) cars_obs32(xs, obs_out + i * 10);
         } else {
             double* xs = x + i * 3;
             float o2 = (float)cos(xs[2]), o3 = (float)sin(xs[2]);
             s32[0] = (float)xs[0];
             s32[1] = (float)xs[1];
             s32[2] = (float)atan2((double)o3, (double)o2);
-            for (int k = 0; k < 3; ++k) sig[k] = (float)0.2;
+            for (int k = 0; k < 3; ++k) {
+                mu[k] = mu_in ? mu_in[i * 3 + k] : 0.0f;
+                sig[k] = sig_in ? sig_in[i * 3 + k] : (float)0.2;
+            }
             uni_rows(s32, u + 2 * i, mu, sig, gamma_b, K, hz, G, h);
             normalize(K + 4, 3, G, h);
             double Pd[3] = {(double)1.0f, (double)1e-2f, (double)1e5f};
@@ -361,9 +395,24 @@ int oracle_safe_step(int mode, int K, const double* hz, double gamma_b, int64_t 
                 u_out[2 * i + c] = a[c];
             }
             uni_env(xs, aux + i, step + i, a, K, hz, rew + i, cost + i, done + i);
+            if (goal_out) goal_out[i] = goal_dist(xs) <= 0.3;
+            if (auto_reset && done[i]) {
+                xs[0] = -2.5; xs[1] = -2.5; xs[2] = 0.0;
+                aux[i] = goal_dist(xs);
+                step[i] = 0;
+            }
+            if (obs_out) uni_obs32(xs, obs_out + i * 7);
         }
     }
     return fails;
+}
+
+/* The fused step with the prior, no auto-reset (bench.py's cpu_baseline). */
+int oracle_safe_step(int mode, int K, const double* hz, double gamma_b, int64_t B, double* x, double* aux,
+                     int32_t* step, const float* u, float* u_out, float* rew, float* cost, uint8_t* done,
+                     int nthreads) {
+    return oracle_safe_step_ex(mode, K, hz, gamma_b, B, x, aux, step, u, NULL, NULL, u_out, rew, cost, done, NULL,
+                               NULL, 0, NULL, nthreads);
 }
 
 int oracle_max_threads(void) {

@@ -350,6 +350,35 @@ int rcbf_env_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int
     return launch_status();
 }
 
+int rcbf_env_step_sync(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
+                       const void* action_host, int32_t action_f64, double* packed_host, int32_t auto_reset,
+                       uint64_t seed, int64_t env_offset, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!packed_host) return RCBF_E_NULL;
+    const int64_t no = prm->mode == RCBF_MODE_SIMULATED_CARS ? Dims<RCBF_MODE_SIMULATED_CARS, 1>::NO
+                                                              : Dims<RCBF_MODE_UNICYCLE, 1>::NO;
+    double* obs64 = packed_host;
+    double* reward = packed_host + B * no;
+    double* cost = reward + B;
+    uint8_t* done = reinterpret_cast<uint8_t*>(cost + B);
+    uint8_t* goal = done + B;
+    int rc = rcbf_env_step(prm, B, x, aux, step, episode, action_host, action_f64, obs64, nullptr, reward, cost, done,
+                           goal, auto_reset, seed, env_offset, stream);
+    if (rc) return rc;
+    return (int)hipStreamSynchronize(stream);
+}
+
+int rcbf_host_alloc(int64_t bytes, void** ptr) {
+    if (!ptr) return RCBF_E_NULL;
+    *ptr = nullptr;
+    if (bytes <= 0) return RCBF_E_BAD_SHAPE;
+    return (int)hipHostMalloc(ptr, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent);
+}
+
+int rcbf_host_free(void* ptr) { return ptr ? (int)hipHostFree(ptr) : 0; }
+
 int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
                    const float* u_rl, const float* mu, const float* sigma, float* obs_out, float* u_out,
                    float* reward, float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
@@ -364,6 +393,30 @@ int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, in
                                           reward, cost, done, goal_met, status_out, fail_flag, auto_reset, seed,
                                           env_offset));
     return launch_status();
+}
+
+int rcbf_safe_step_seq(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux, int32_t* step,
+                       uint32_t* episode, const float* const* u_rl_seq, int32_t n_u_rl, const float* mu,
+                       const float* sigma, float* obs_out, float* u_out, float* reward, float* cost, uint8_t* done,
+                       uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag, int32_t auto_reset, uint64_t seed,
+                       int64_t env_offset, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0 || K < 0 || n_u_rl < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0 || K == 0) return 0;
+    if (!u_rl_seq || n_u_rl == 0) return RCBF_E_NULL;
+    for (int32_t j = 0; j < n_u_rl; ++j)
+        if (!u_rl_seq[j]) return RCBF_E_NULL;
+    if (!x || !aux || !step || !obs_out || !u_out || !reward || !cost || !done) return RCBF_E_NULL;
+    if ((((uintptr_t)obs_out) & 7) || (((uintptr_t)x) & 15)) return RCBF_E_BAD_SHAPE;
+    RCBF_DISPATCH(prm, {
+        for (int32_t j = 0; j < K; ++j) {
+            hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0, stream,
+                               *prm, B, x, aux, step, episode, u_rl_seq[j % n_u_rl], mu, sigma, obs_out, u_out,
+                               reward, cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset);
+            if (int e = launch_status()) return e;
+        }
+    });
+    return 0;
 }
 
 int rcbf_safe_rollout(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux, int32_t* step,

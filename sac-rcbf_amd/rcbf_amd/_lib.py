@@ -22,7 +22,7 @@ SOLVER_PDIPM = 1
 SOLVER_GI = 2
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NONFINITE = 0, 1, 2, 3
 MAX_HAZARDS = 8
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL"}
 
@@ -87,6 +87,11 @@ SIGNATURES = {
     "rcbf_env_step": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
     "rcbf_safe_step": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
     "rcbf_safe_rollout": [_PRM, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _P],
+    "rcbf_safe_step_seq": [_PRM, _I64, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                           _I32, _U64, _I64, _P],
+    "rcbf_env_step_sync": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _I32, _U64, _I64, _P],
+    "rcbf_host_alloc": [_I64, ctypes.POINTER(ctypes.c_void_p)],
+    "rcbf_host_free": [_P],
     "rcbf_version": [],
     "rcbf_abi_version": [],
     "rcbf_params_size": [],
@@ -117,8 +122,37 @@ def load():
     lib.rcbf_gp_workspace_floats.restype = ctypes.c_int64
     if lib.rcbf_abi_version() != ABI_VERSION or lib.rcbf_params_size() != ctypes.sizeof(RcbfParams):
         raise RuntimeError("librcbf_hip.so ABI mismatch (rebuild with `python __graft_entry__.py build`)")
+    _bind_fast(lib)
     _lib = lib
     return lib
+
+
+FAST_ENTRY_POINTS = ("rcbf_safe_step", "rcbf_safe_step_seq", "rcbf_env_step_sync")
+_fast = None
+
+
+def _bind_fast(lib):
+    """Point the CPython binding (csrc/rcbf_pyfast.cpp, optional) at the entry
+    points of THIS library copy -- the one ctypes loaded, RCBF_HIP_LIB
+    included -- so both bindings always launch the same code."""
+    global _fast
+    try:
+        from . import _rcbf_fast
+    except ImportError:
+        _fast = None
+        return
+    _rcbf_fast.bind(*(entry_address(lib, n) for n in FAST_ENTRY_POINTS))
+    _fast = _rcbf_fast
+
+
+def entry_address(lib, name):
+    return ctypes.cast(getattr(lib, name), ctypes.c_void_p).value
+
+
+def fast():
+    """The CPython binding bound to the loaded library, or None if not built."""
+    load()
+    return _fast
 
 
 def check(rc, what):

@@ -25,10 +25,14 @@ import torch
 from . import _lib
 from .params import make_params
 
-try:  # optional CPython binding of rcbf_safe_step (built next to librcbf_hip.so by build())
-    from . import _rcbf_fast as _fast
-except ImportError:
-    _fast = None
+# The optional CPython binding (csrc/rcbf_pyfast.cpp), bound by _lib.load() to
+# the library ctypes loaded.  Tests set _fast = None to force the ctypes path.
+_FAST_DEFAULT = object()
+_fast = _FAST_DEFAULT
+
+
+def _fast_binding():
+    return _lib.fast() if _fast is _FAST_DEFAULT else _fast
 
 try:  # keep gym's types when gym is installed (it is not in this image)
     import gym as _gym
@@ -231,36 +235,105 @@ class BatchedEnv:
         The ctypes argument list is cached per (layer, outputs tensors,
         auto_reset): an eager call then costs one data_ptr per changing
         input, so the host keeps pace with the ~4 us kernel."""
-        B, d = self.num_envs, self.device
         o = outputs if outputs is not None else self.make_outputs()
+        u = self._u_arg(u_rl)
+        mean, sigma = self._prior_arg(mean, "mean"), self._prior_arg(sigma, "sigma")
+        args = self._step_args(layer, o, auto_reset)
+        args[6] = u.data_ptr()
+        args[7] = 0 if mean is None else mean.data_ptr()
+        args[8] = 0 if sigma is None else sigma.data_ptr()
+        args[20] = torch._C._cuda_getCurrentRawStream(self.device.index)
+        fast = _fast_binding()
+        if fast is not None:  # CPython binding (csrc/rcbf_pyfast.cpp): ~1 us instead of ~4 us through ctypes
+            rc = fast.safe_step(*args)
+        else:
+            rc = _lib.load().rcbf_safe_step(ctypes.byref(layer._prm), self.num_envs, *[a or None for a in args[2:17]],
+                                            *args[17:20], args[20] or None)
+        _lib.check(rc, "rcbf_safe_step")
+        return self.obs, o["reward"], o["done"], o
+
+    def safe_step_seq(self, u_rl_seq, layer, mean=None, sigma=None, auto_reset=True, outputs=None, steps=None):
+        """`steps` fused safe steps (default len(u_rl_seq)) issued from ONE host
+        call (rcbf_safe_step_seq): step j uses u_rl_seq[j % len(u_rl_seq)],
+        each (B, n_u) f32 on this device.  Every step is its own launch of the
+        fused kernel, exactly as `steps` calls of safe_step; the outputs hold
+        the last step's values."""
+        o = outputs if outputs is not None else self.make_outputs()
+        us = [self._u_arg(u) for u in u_rl_seq]
+        if not us:
+            raise ValueError("u_rl_seq is empty")
+        K = len(us) if steps is None else int(steps)
+        mean, sigma = self._prior_arg(mean, "mean"), self._prior_arg(sigma, "sigma")
+        a = list(self._step_args(layer, o, auto_reset))
+        stream = torch._C._cuda_getCurrentRawStream(self.device.index)
+        ptrs = [t.data_ptr() for t in us]
+        fast = _fast_binding()
+        tail = a[9:17] + a[17:20]
+        if fast is not None:
+            rc = fast.safe_step_seq(a[0], a[1], K, *a[2:6], ptrs, 0 if mean is None else mean.data_ptr(),
+                                    0 if sigma is None else sigma.data_ptr(), *tail, stream)
+        else:
+            arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+            rc = _lib.load().rcbf_safe_step_seq(ctypes.byref(layer._prm), self.num_envs, K,
+                                                *[v or None for v in a[2:6]], arr, len(ptrs),
+                                                None if mean is None else mean.data_ptr(),
+                                                None if sigma is None else sigma.data_ptr(),
+                                                *[v or None for v in a[9:17]], *a[17:20], stream or None)
+        _lib.check(rc, "rcbf_safe_step_seq")
+        return self.obs, o["reward"], o["done"], o
+
+    def _u_arg(self, u_rl):
+        B, d = self.num_envs, self.device
         u = u_rl if (torch.is_tensor(u_rl) and u_rl.dtype == torch.float32 and u_rl.is_contiguous()
                      and u_rl.device == d) else torch.as_tensor(u_rl, dtype=torch.float32, device=d).contiguous()
         if u.shape != (B, self.n_u):
             raise ValueError(f"u_rl must be ({B}, {self.n_u}), got {tuple(u.shape)}")
-        mean, sigma = self._prior_arg(mean, "mean"), self._prior_arg(sigma, "sigma")
-        key =(id(layer), auto_reset, tuple(map(id, o.values())))
-        ent = self._ss_cache.get(key) if hasattr(self, "_ss_cache") else None
-        if ent is None or ent[0] is not layer or ent[1] is not o:
+        return u
+
+    def _check_layer(self, layer):
+        """The fused kernel runs the env physics with the LAYER's params: they
+        must describe this env (mode, hazards, gains), or it would index the
+        state buffers with the wrong dimension."""
+        p, q = layer._prm, self._prm_env
+        same = (p.mode == q.mode and p.num_hazards == q.num_hazards and p.kp == q.kp and p.k_brake == q.k_brake
+                and p.hazards_radius == q.hazards_radius
+                and all(p.hazards_xy[k] == q.hazards_xy[k] for k in range(2 * q.num_hazards)))
+        if not same:
+            raise ValueError("the CBF layer was built for a different env (dynamics mode, hazards or gains differ)")
+
+    def _check_outputs(self, o):
+        B, d = self.num_envs, self.device
+        want = {"u": ((B, self.n_u), torch.float32), "reward": ((B,), torch.float32),
+                "cost": ((B,), torch.float32), "done": ((B,), torch.uint8), "goal_met": ((B,), torch.uint8)}
+        for k, (shape, dt) in want.items():
+            t = o.get(k)
+            if t is None and k == "goal_met":
+                continue
+            if not (torch.is_tensor(t) and tuple(t.shape) == shape and t.dtype == dt and t.device == d
+                    and t.is_contiguous()):
+                raise ValueError(f"outputs[{k!r}] must be a contiguous {dt} tensor of shape {shape} on {d} "
+                                 "(use make_outputs())")
+
+    def _step_args(self, layer, o, auto_reset):
+        """The argument list of rcbf_safe_step (u_rl/mean/sigma/stream slots
+        filled per call), cached per (layer params, outputs, auto_reset, RNG
+        seed, shard offset); layer and outputs are validated when an entry is
+        built, so the check stays off the per-step path."""
+        key = (id(layer), id(layer._prm), bool(auto_reset), self._rng_seed(), self.env_offset,
+               tuple(map(id, o.values())))
+        ent = getattr(self, "_ss_cache", {}).get(key)
+        if ent is None or ent[0] is not layer or ent[1] is not o or ent[4] is not layer._prm:
+            self._check_layer(layer)
+            self._check_outputs(o)
             self._ss_cache = {}
 
             def p(t):
                 return 0 if t is None else t.data_ptr()
-            args = [ctypes.addressof(layer._prm), B, p(self.x), p(self.aux), p(self.step_count), p(self.episode),
-                    0, 0, 0, p(self.obs), p(o["u"]), p(o["reward"]), p(o["cost"]), p(o["done"]),
+            args = [ctypes.addressof(layer._prm), self.num_envs, p(self.x), p(self.aux), p(self.step_count),
+                    p(self.episode), 0, 0, 0, p(self.obs), p(o["u"]), p(o["reward"]), p(o["cost"]), p(o["done"]),
                     p(o.get("goal_met")), 0, p(self.fail_flag), int(auto_reset), self._rng_seed(), self.env_offset, 0]
-            ent = self._ss_cache[key] = (layer, o, args, [t for t in o.values() if t is not None])
-        args = ent[2]
-        args[6] = u.data_ptr()
-        args[7] = 0 if mean is None else mean.data_ptr()
-        args[8] = 0 if sigma is None else sigma.data_ptr()
-        args[20] = torch._C._cuda_getCurrentRawStream(d.index)
-        if _fast is not None:  # CPython binding (csrc/rcbf_pyfast.cpp): ~1 us instead of ~4 us through ctypes
-            rc = _fast.safe_step(*args)
-        else:
-            rc = _lib.load().rcbf_safe_step(ctypes.byref(layer._prm), B, *[a or None for a in args[2:17]],
-                                            *args[17:20], args[20] or None)
-        _lib.check(rc, "rcbf_safe_step")
-        return self.obs, o["reward"], o["done"], o
+            ent = self._ss_cache[key] = (layer, o, args, [t for t in o.values() if t is not None], layer._prm)
+        return ent[2]
 
     def make_outputs(self):
         B, d = self.num_envs, self.device
@@ -344,44 +417,68 @@ class _SingleEnv(_EnvBase):
     def unwrapped(self):
         return self
 
+    def _host_io(self):
+        """Pinned, device-coherent host buffers the step kernel reads the
+        action from and writes its results to (rcbf_host_alloc), plus the
+        cached argument list of rcbf_env_step_sync."""
+        io = getattr(self, "_io", None)
+        if io is not None:
+            return io
+        lib, b, n_o = _lib.load(), self._b, self.n_o
+        nbytes = 8 * (n_o + 2) + 2 + 16 + 16  # packed outputs | f32 action (2) | f64 action (2)
+        p = ctypes.c_void_p()
+        _lib.check(lib.rcbf_host_alloc(nbytes + 16, ctypes.byref(p)), "rcbf_host_alloc")
+        base = (p.value + 15) & ~15
+        act = 8 * (n_o + 2) + 16
+        io = {"raw": p.value, "base": base,
+              "pk": np.ctypeslib.as_array((ctypes.c_double * (n_o + 2)).from_address(base)),
+              "flags": np.ctypeslib.as_array((ctypes.c_uint8 * 2).from_address(base + 8 * (n_o + 2))),
+              "a32": np.ctypeslib.as_array((ctypes.c_float * 2).from_address(base + act)),
+              "a64": np.ctypeslib.as_array((ctypes.c_double * 2).from_address(base + act + 16)),
+              "a32p": base + act, "a64p": base + act + 16,
+              "args": [ctypes.addressof(b._prm_env), 1, b.x.data_ptr(), b.aux.data_ptr(), b.step_count.data_ptr(),
+                       b.episode.data_ptr(), 0, 0, base, 0, b._rng_seed(), b.env_offset, 0]}
+        self._io = io
+        return io
+
+    def __del__(self):
+        io = getattr(self, "_io", None)
+        if io is not None and _lib is not None:
+            try:
+                _lib.load().rcbf_host_free(io["raw"])
+            except Exception:
+                pass
+
     def step(self, action):
-        """One env step with ONE device->host transfer: the kernel writes
-        obs (fp64), reward, cost, done and goal_met into one packed device
-        row, which is copied to pinned host memory and synchronised once (the
-        action goes up through a pinned buffer without a sync)."""
+        """One env step in ONE host call (rcbf_env_step_sync): the kernel
+        reads the action from pinned host memory, steps the device-resident
+        env and writes obs (fp64), reward, cost, done and goal_met straight
+        into pinned host memory; the call returns once the stream is done."""
         a = np.asarray(action)
         if a.dtype not in (np.float32, np.float64):
             a = a.astype(np.float32)
         f64 = a.dtype == np.float64
-        b = self._b
-        if not hasattr(self, "_pk"):
-            n_o, n_u, d = self.n_o, self.n_u, b.device
-            self._pk = torch.zeros(n_o + 4, dtype=torch.float64, device=d)
-            self._pkh = torch.zeros(n_o + 4, dtype=torch.float64, pin_memory=True)
-            self._pkb = self._pkh.view(torch.uint8)
-            self._ah = {False: torch.zeros(n_u, dtype=torch.float32, pin_memory=True),
-                        True: torch.zeros(n_u, dtype=torch.float64, pin_memory=True)}
-            self._ad = {False: torch.zeros(n_u, dtype=torch.float32, device=d),
-                        True: torch.zeros(n_u, dtype=torch.float64, device=d)}
+        io = self._host_io()
         n_o = self.n_o
-        ah, ad = self._ah[f64], self._ad[f64]
-        ah.numpy()[:] = a.reshape(-1)
-        ad.copy_(ah, non_blocking=True)
-        base = self._pk.data_ptr()
-        at = (lambda k: ctypes.c_void_p(base + 8 * k))
-        rc = _lib.load().rcbf_env_step(ctypes.byref(b._prm_env), 1, _lib.ptr(b.x), _lib.ptr(b.aux),
-                                       _lib.ptr(b.step_count), _lib.ptr(b.episode), _lib.ptr(ad), int(f64),
-                                       at(0), _lib.ptr(b.obs), at(n_o), at(n_o + 1), at(n_o + 2), at(n_o + 3),
-                                       0, b._rng_seed(), b.env_offset, b._stream())
-        _lib.check(rc, "rcbf_env_step")
-        self._pkh.copy_(self._pk, non_blocking=True)
-        torch.cuda.current_stream(b.device).synchronize()
-        h = self._pkh.numpy()
-        obs = h[:n_o].copy()
-        r = np.float64(h[n_o]) if f64 else np.float32(h[n_o])
-        done = bool(self._pkb[8 * (n_o + 2)])
-        goal = bool(self._pkb[8 * (n_o + 3)])
-        return obs, r, done, self._info_host(float(h[n_o + 1]), goal)
+        if f64:
+            io["a64"][:self.n_u] = a.reshape(-1)
+        else:
+            io["a32"][:self.n_u] = a.reshape(-1)
+        args = io["args"]
+        args[6] = io["a64p"] if f64 else io["a32p"]
+        args[7] = int(f64)
+        args[12] = torch._C._cuda_getCurrentRawStream(self._b.device.index)
+        fast = _fast_binding()
+        if fast is not None:
+            rc = fast.env_step_sync(*args)
+        else:
+            rc = _lib.load().rcbf_env_step_sync(ctypes.byref(self._b._prm_env), 1, *args[2:10], args[10], args[11],
+                                                args[12] or None)
+        _lib.check(rc, "rcbf_env_step_sync")
+        pk = io["pk"]
+        obs = pk[:n_o].copy()
+        r = np.float64(pk[n_o]) if f64 else np.float32(pk[n_o])
+        return obs, r, bool(io["flags"][0]), self._info_host(float(pk[n_o + 1]), bool(io["flags"][1]))
 
     def render(self, mode="human", close=False):
         print("Ep_step = {}, \tState = {}".format(self.episode_step, self.state))

@@ -145,6 +145,7 @@ def test_fast_binding_loads_and_validates():
     next to librcbf_hip.so and forwards to the same C-ABI (argument checks run
     before any launch, so this needs no GPU)."""
     from rcbf_amd import _lib, _rcbf_fast
+    _lib.load()
     p = _lib.RcbfParams()
     p.mode = _lib.MODE_SIMULATED_CARS
     a = ctypes.addressof(p)
@@ -154,3 +155,37 @@ def test_fast_binding_loads_and_validates():
     assert _rcbf_fast.safe_step(a, 4, *([0] * 19)) == 1001       # bad mode
     with pytest.raises(TypeError):
         _rcbf_fast.safe_step(a, 4)
+    p.mode = _lib.MODE_SIMULATED_CARS
+    assert _rcbf_fast.safe_step_seq(a, 4, 3, 0, 0, 0, 0, [0], *([0] * 14)) == 1003  # NULL u_rl pointer
+    assert _rcbf_fast.safe_step_seq(a, 0, 3, 0, 0, 0, 0, [0], *([0] * 14)) == 0     # empty batch
+    assert _rcbf_fast.env_step_sync(a, 1, *([0] * 11)) == 1003                      # NULL host block
+    with pytest.raises(ValueError):
+        _rcbf_fast.safe_step_seq(a, 4, 3, 0, 0, 0, 0, [], *([0] * 14))
+
+
+def test_fast_binding_follows_the_library_override(tmp_path):
+    """With RCBF_HIP_LIB pointing at another copy of the library, the CPython
+    binding calls into THAT copy (the one ctypes loaded), not a second,
+    default copy (variant benches must measure the variant)."""
+    import shutil
+    import subprocess
+    import sys
+    from rcbf_amd import _lib
+    variant = tmp_path / "librcbf_variant.so"
+    shutil.copy(_lib.LIB_PATH, variant)
+    code = (
+        "import ctypes, sys\n"
+        f"sys.path[:0] = [{os.path.join(ROOT, 'sac-rcbf_amd')!r}]\n"
+        "from rcbf_amd import _lib\n"
+        "lib = _lib.load()\n"
+        "got = _lib.fast().bound()\n"
+        "want = tuple(_lib.entry_address(lib, n) for n in _lib.FAST_ENTRY_POINTS)\n"
+        "assert got == want, (got, want)\n"
+        "maps = [l.split() for l in open('/proc/self/maps') if l.rstrip().endswith('librcbf_variant.so')]\n"
+        "spans = [tuple(int(v, 16) for v in m[0].split('-')) for m in maps]\n"
+        "assert all(any(lo <= a < hi for lo, hi in spans) for a in got), 'binding points outside the variant'\n"
+        "assert not any(l.rstrip().endswith('/librcbf_hip.so') for l in open('/proc/self/maps'))\n"
+        "print('ok')\n")
+    env = dict(os.environ, RCBF_HIP_LIB=str(variant))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

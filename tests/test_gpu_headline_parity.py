@@ -1,0 +1,195 @@
+"""GPU parity at the sizes bench.py measures: the exact benchmark workload
+(bench.init_states start states, bench's seeds, u_RL ~ U[-1, 1], prior
+mean/sigma, auto-reset ON) stepped by the fused HIP kernel through the C-ABI,
+and every step checked against the C oracle (oracle/rcbf_oracle.c) from the
+same pre-step state ("teacher forcing": each step is compared from identical
+inputs, so a difference cannot hide behind trajectory divergence).
+
+Per step, per env (north star: safe action within 1e-4 relative):
+  * safe action u:       |du| <= 1e-4 max(1, |u|)
+  * env state, aux, step: <= 1e-9 relative (exact for step), except the
+    velocities of a cars env that auto-reset in this step: the reset draw is
+    0.5 * Box-Muller(Philox4x32-10(seed, global env, episode)) with the
+    device's hardware fp32 log2/cos, checked against the oracle's restatement
+    (oracle.normal_draw) to 1e-5 absolute (positions, t and step exact)
+  * cost, done, goal_met: exact;  reward: cars bit-exact (fp32, same
+    operations), unicycle <= 1e-6 absolute (an fp64 difference cast to fp32)
+  * observation rows (fp32): cars <= 1 ulp-relative 1e-6, unicycle 1e-6.
+
+Configs: cars B = 65536 (the headline), unicycle k = 3 and 5 (the
+reference's default hazard count) at B = 65536, cars B = 262144 (config 4),
+and config 4's 8-way shard (8 x 32768 envs with env_offset = r x 32768)
+reproducing the unsharded batch bit for bit, resets included.
+"""
+import numpy as np
+import pytest
+import torch
+
+import bench
+from oracle import c_oracle as C
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+class Args:
+    cuda = True
+
+
+def _make(mode, B, hazards=3, seed=1234, offset=0):
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+    dev = torch.device("cuda", 0)
+    if mode == "SimulatedCars":
+        env = BatchedSimulatedCarsEnv(B, device=dev, seed=seed, env_offset=offset)
+    else:
+        env = BatchedUnicycleEnv(B, device=dev, seed=seed, env_offset=offset,
+                                 hazards_locations=env_hazards(hazards))
+    return env, CBFQPLayer(env, Args(), gamma_b=20.0)
+
+
+def env_hazards(k):
+    from rcbf_amd.envs import _EnvSpec
+    return _EnvSpec("Unicycle").hazards_locations[:k]
+
+
+def _snapshot(env):
+    return (np.ascontiguousarray(env.state.cpu().numpy()), env.aux.cpu().numpy().copy(),
+            env.step_count.cpu().numpy().astype(np.int32), env.episode.cpu().numpy().astype(np.int64))
+
+
+def _rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.abs(a - b) / np.maximum(1.0, np.abs(b))
+
+
+def _worst(name, err, tol, extra=""):
+    bad = np.argwhere(err > tol)
+    assert bad.size == 0, f"{name}: {bad.shape[0]} entries above {tol}, worst {err.max():.3e} at {bad[0]} {extra}"
+
+
+def run_teacher_forced(mode, B, steps, hazards=3, pool=8):
+    """Run `steps` fused steps of bench's workload; compare each with the C
+    oracle started from the GPU's pre-step state.  Returns counts."""
+    env, layer = _make(mode, B, hazards)
+    gen = torch.Generator(device=env.device)
+    gen.manual_seed(1000)
+    bench.init_states(env, gen, mode)
+    us = [(torch.rand(B, env.n_u, device=env.device, generator=gen) * 2 - 1).contiguous() for _ in range(pool)]
+    outs = env.make_outputs()
+    hz = env.hazards_locations if mode == "Unicycle" else None
+    idx = env.env_offset + np.arange(B)
+    n_reset = n_active = 0
+    for k in range(steps):
+        x, aux, st, ep = _snapshot(env)
+        u = us[k % pool]
+        env.safe_step(u, layer, outputs=outs)
+        torch.cuda.synchronize()
+        u_h = u.cpu().numpy()
+        noise = 0.5 * O.normal_draw(env._rng_seed(), idx, ep + 1) if mode == "SimulatedCars" else None
+        ref = C.safe_step_ex(mode, x, aux, st, u_h, 20.0, hazards=hz, auto_reset=True, reset_noise=noise)
+        assert ref["fails"] == 0
+        env.check_failures()
+        tag = f"{mode} B={B} step {k}"
+        _worst(f"{tag} u", _rel(outs["u"].cpu().numpy(), ref["u"]), 1e-4)
+        done = outs["done"].cpu().numpy()
+        assert np.array_equal(done, ref["done"]), f"{tag} done"
+        assert np.array_equal(outs["cost"].cpu().numpy(), ref["cost"]), f"{tag} cost"
+        rg, rr = outs["reward"].cpu().numpy(), ref["reward"]
+        if mode == "SimulatedCars":
+            assert np.array_equal(rg, rr), f"{tag} reward"
+        else:
+            _worst(f"{tag} reward", np.abs(rg.astype(np.float64) - rr), 1e-6)
+            assert np.array_equal(outs["goal_met"].cpu().numpy(), ref["goal"]), f"{tag} goal_met"
+        xg, ag, sg, _ = _snapshot(env)
+        assert np.array_equal(sg, st), f"{tag} step counter"
+        _worst(f"{tag} aux", _rel(ag, aux), 1e-9)
+        reset = done.astype(bool)
+        if mode == "SimulatedCars":
+            vel = np.zeros(xg.shape[1], bool)
+            vel[1::2] = True
+            err = _rel(xg, x)
+            _worst(f"{tag} state", err[~reset], 1e-9)
+            _worst(f"{tag} reset positions", np.abs(xg[reset][:, ~vel] - x[reset][:, ~vel]), 0.0)
+            _worst(f"{tag} reset draw", np.abs(xg[reset][:, vel] - x[reset][:, vel]), 1e-5)
+            ob = _rel(env.obs.cpu().numpy(), ref["obs"])
+            _worst(f"{tag} obs", ob[~reset], 1e-6)
+        else:
+            _worst(f"{tag} state", _rel(xg, x), 1e-9)
+            _worst(f"{tag} obs", _rel(env.obs.cpu().numpy(), ref["obs"]), 1e-6)
+        n_reset += int(reset.sum())
+        n_active += int((outs["u"].cpu().numpy() != u_h).any(1).sum())
+    return {"resets": n_reset, "filter_active": n_active, "env_steps": B * steps}
+
+
+def test_headline_cars_B65536_vs_oracle():
+    r = run_teacher_forced("SimulatedCars", 65536, 24)
+    assert r["resets"] > 2000           # ~B x 24 / 300 episodes end in the window
+    assert r["filter_active"] > 0.05 * r["env_steps"]  # the filter changes ~10 % of the actions here
+
+
+@pytest.mark.parametrize("k", [3, 5])
+def test_headline_unicycle_B65536_vs_oracle(k):
+    r = run_teacher_forced("Unicycle", 65536, 24, hazards=k)
+    assert r["resets"] > 500
+    assert r["filter_active"] > 0.02 * r["env_steps"]
+
+
+def test_config4_cars_B262144_vs_oracle():
+    r = run_teacher_forced("SimulatedCars", 262144, 8)
+    assert r["resets"] > 2000
+
+
+def test_config4_eight_way_shard_reproduces_the_whole_batch():
+    """SimulatedCars batch = 262144 sharded 8 ways (config 4): the shards
+    (env_offset = r x 32768, as bench.py / shard.env_offset give each rank)
+    stepped with their slices of u_RL equal the unsharded batch bit for bit
+    after 40 steps, auto-resets and their Philox reset draws included."""
+    B, R, T = 262144, 8, 40
+    full, lf = _make("SimulatedCars", B)
+    gen = torch.Generator(device=full.device)
+    gen.manual_seed(1000)
+    bench.init_states(full, gen, "SimulatedCars")
+    x0, a0, s0 = full.state.clone(), full.aux.clone(), full.step_count.clone()
+    per = B // R
+    shards = []
+    for r in range(R):
+        e, l = _make("SimulatedCars", per, offset=r * per)
+        e.load_state(x0[r * per:(r + 1) * per], a0[r * per:(r + 1) * per], s0[r * per:(r + 1) * per])
+        e.episode.copy_(full.episode[r * per:(r + 1) * per])
+        shards.append((e, l))
+    us = [(torch.rand(B, 1, device=full.device, generator=gen) * 2 - 1).contiguous() for _ in range(8)]
+    for k in range(T):
+        _, rf, df, of = full.safe_step(us[k % 8], lf)
+        for r, (e, l) in enumerate(shards):
+            _, rs, ds, os_ = e.safe_step(us[k % 8][r * per:(r + 1) * per].contiguous(), l)
+            sl = slice(r * per, (r + 1) * per)
+            assert torch.equal(os_["u"], of["u"][sl]) and torch.equal(rs, rf[sl]) and torch.equal(ds, df[sl])
+            assert torch.equal(e.obs, full.obs[sl])
+    for r, (e, _) in enumerate(shards):
+        sl = slice(r * per, (r + 1) * per)
+        assert torch.equal(e.state, full.state[sl]) and torch.equal(e.episode, full.episode[sl])
+        e.check_failures()
+    assert int(full.episode.max().item()) >= 2  # episodes rolled over inside the window
+    full.check_failures()
+
+
+def test_safe_step_seq_equals_single_steps():
+    """rcbf_safe_step_seq (K launches from one host call, u_RL cycled from a
+    pointer list) == K safe_step calls, bit for bit."""
+    B, K = 65536, 30
+    a, la = _make("SimulatedCars", B)
+    b, lb = _make("SimulatedCars", B)
+    gen = torch.Generator(device=a.device)
+    gen.manual_seed(3)
+    bench.init_states(a, gen, "SimulatedCars")
+    b.load_state(a.state, a.aux, a.step_count)
+    b.episode.copy_(a.episode)
+    us = [(torch.rand(B, 1, device=a.device, generator=gen) * 2 - 1).contiguous() for _ in range(7)]
+    oa, ob = a.make_outputs(), b.make_outputs()
+    a.safe_step_seq(us, la, outputs=oa, steps=K)
+    for k in range(K):
+        b.safe_step(us[k % 7], lb, outputs=ob)
+    assert torch.equal(a.state, b.state) and torch.equal(a.step_count, b.step_count)
+    assert torch.equal(a.obs, b.obs) and all(torch.equal(oa[k], ob[k]) for k in oa)

@@ -414,7 +414,8 @@ def test_fast_binding_matches_ctypes_path(mode, monkeypatch):
     ctypes launch the same C-ABI entry point: bit-identical trajectories, with
     and without a disturbance prior, auto-resets included, on a side stream."""
     import rcbf_amd.envs as E
-    assert E._fast is not None, "_rcbf_fast extension not built (run __graft_entry__.build())"
+    from rcbf_amd import _lib
+    assert _lib.fast() is not None, "_rcbf_fast extension not built (run __graft_entry__.build())"
     B = 1000
     rng = np.random.default_rng(5)
     us = [dev(rng.uniform(-1, 1, (B, 1 if mode == "SimulatedCars" else 2))) for _ in range(12)]
@@ -454,6 +455,21 @@ def test_fast_binding_matches_ctypes_path(mode, monkeypatch):
         e.safe_step(torch.zeros(4, 1, device="cuda"), lay)
     e.safe_step(u, lay, mean=torch.zeros(8, 10, dtype=torch.float64, device="cuda"))  # converted to fp32
     e.check_failures()
+    # a layer built for another env is refused (the kernel runs the env physics with the layer's params)
+    uni = E.BatchedUnicycleEnv(8, seed=1, hazards_locations=O.UNI["hazards"][:3])
+    with pytest.raises(ValueError, match="different env"):
+        uni.safe_step(torch.zeros(8, 2, device="cuda"), lay)
+    uni5 = E.BatchedUnicycleEnv(8, seed=1)
+    with pytest.raises(ValueError, match="different env"):
+        uni.safe_step(torch.zeros(8, 2, device="cuda"), _layer(uni5, 20.0))
+    # malformed caller-supplied outputs are refused when the argument cache is built
+    bad = e.make_outputs()
+    bad["reward"] = torch.empty(8, dtype=torch.float64, device="cuda")
+    with pytest.raises(ValueError, match="outputs"):
+        e.safe_step(u, lay, outputs=bad)
+    small = E.BatchedSimulatedCarsEnv(4, seed=1).make_outputs()
+    with pytest.raises(ValueError, match="outputs"):
+        e.safe_step(u, lay, outputs=small)
 
 
 def test_rollout_matches_single_steps():
