@@ -36,6 +36,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 #   unicycle: read  x 24 + last_dist 8 + step 4 + u_RL 8                 =  44
 #             write x 24 + ld 8 + step 4 + obs 28 + u 8 + r 4 + c 4 + done 1 + goal 1 = 82
 BYTES_PER_STEP = {"SimulatedCars": 96 + 145, "Unicycle": 44 + 82}
+# with per-env mean/sigma tensors (--prior tensor) the kernel also reads what
+# the rows use: cars sigma[5], sigma[7], sigma[9] (the cars rows ignore mu,
+# diff_cbf_qp.py:298-299) = 12 B; unicycle mu 12 + sigma 12 = 24 B
+PRIOR_TENSOR_BYTES = {"SimulatedCars": 12, "Unicycle": 24}
+
+
+def bytes_per_step(args):
+    return BYTES_PER_STEP[args.env] + (PRIOR_TENSOR_BYTES[args.env] if args.prior == "tensor" else 0)
 
 
 def parse():
@@ -56,6 +64,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extra", action="store_true", help="also time the K-step rollout kernel and big batches")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (for PMC counter passes)")
+    ap.add_argument("--prior", default="prior", choices=["prior", "tensor"],
+                    help="prior: the DynamicsModel prior in-kernel (before any GP fit); tensor: per-env mean/sigma "
+                         "tensors read from HBM (after the GP fit)")
+    ap.add_argument("--cpu-dry-run", action="store_true",
+                    help="CPU/gloo plumbing check of the launcher (no kernel, no measurement)")
     ap.add_argument("--launch", default="graph", choices=["graph", "seq"],
                     help="graph: hipGraph replays of --graph-steps fused steps; seq: the K launches issued from "
                          "one host call (rcbf_safe_step_seq)")
@@ -137,12 +150,12 @@ def cpu_reference_mode(env_name, hazards, seconds):
                       f"{its / n:.1f} iterations per step), {n} steps x {B} envs in {el:.1f} s on {threads} threads"}
 
 
-def pmc_traffic(env_name, B):
+def pmc_traffic(env_name, B, hazards=3, prior="prior"):
     """HBM bytes per launch of k_safe_step from the committed rocprofv3 PMC
     passes (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, gfx950
     corrections) for this exact workload, newest round first; None if absent."""
     import glob
-    short = "cars" if env_name == "SimulatedCars" else "unicycle3"
+    short = ("cars" if env_name == "SimulatedCars" else f"unicycle{hazards}") + ("_tensorprior" if prior == "tensor" else "")
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{short}_B{B}.json")),
                        reverse=True):
         try:
@@ -179,34 +192,176 @@ def init_states(env, gen, env_name):
     torch.cuda.synchronize()
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` run as a plain process: start N rank processes of
+    this same script BEFORE anything touches the GPU (this parent never
+    initialises HIP), one per GPU, with the torchrun environment (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT).  Rank
+    0 inherits stdout and prints the JSON line.  If a rank fails the others
+    are stopped; returns the first non-zero exit status (0 if all succeed)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+class _DryRun:
+    """--cpu-dry-run: the launcher, rendezvous, barrier / max-over-ranks and
+    the JSON line, on the CPU with gloo and no kernel (the timed region is an
+    empty loop).  For the multi-process CPU tests only; never a measurement."""
+
+    def __init__(self, B, n_u):
+        self.num_envs, self.n_u = B, n_u
+
+    def replay(self):
+        pass
+
+    def check_failures(self):
+        pass
+
+
 def main():
     args = parse()
     from rcbf_amd import shard
     rank, local, world = shard.world_info()
+    if world == 1 and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.gpus != world and args.gpus != 1:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
     if args.scaling == "strong":
         if args.batch % world:
             raise SystemExit("--scaling strong needs --batch divisible by the GPU count")
         args.batch //= world
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    B = args.batch
+    if args.cpu_dry_run:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+        S, reps = args.steps, 1
+        graph = env = _DryRun(B, 1 if args.env == "SimulatedCars" else 2)
+        active_frac, layer = 0.0, None
+        sync = lambda: None  # noqa: E731
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+        env, layer, graph, S, active_frac = setup_gpu(args, dev, rank, B)
+        reps = args.steps // S
+        sync = torch.cuda.synchronize
 
-    from rcbf_amd import _lib
+    if not args.cpu_dry_run:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    shard.barrier(world)
+    sync()
+    t0 = time.perf_counter()
+    if not args.cpu_dry_run:
+        ev0.record()
+    for _ in range(reps):
+        graph.replay()
+    if not args.cpu_dry_run:
+        ev1.record()
+    sync()
+    shard.barrier(world)
+    el = time.perf_counter() - t0
+    # per fused-step launch, HIP events on the launch stream (torch's current stream)
+    kern_ms = ev0.elapsed_time(ev1) / args.steps if not args.cpu_dry_run else 0.0
+    env.check_failures()
+    el = shard.max_over_ranks(el, world, dev)
+    kern_ms = shard.max_over_ranks(kern_ms, world, dev)
+    value = shard.whole_job_rate(world, B, args.steps, el)
+    bps = bytes_per_step(args)
+    achieved = B * bps / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(args.env, B, args.hazards, args.prior)
+    extra = {}
+    if args.extra and rank == 0 and not args.cpu_dry_run:
+        extra = extra_measurements(env, layer, dev, args)
+    hz = f"{args.hazards}-hazard " if args.env == "Unicycle" else ""
+    launch = ("no kernel (CPU dry run)" if args.cpu_dry_run else "eager launches" if args.no_graph
+              else f"{S} launches from one host call" if args.launch == "seq" else f"hipGraph of {S} steps")
+    rec = {
+        "metric": "safe env steps/sec (dynamics+CBF-QP) at batch 65536, 1/2/4/8 MI355X",
+        "value": round(value, 1),
+        "unit": "safe env steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "f32 rows / f64 QP / f64 env",
+        "data": ("dry run: launcher and collectives only, no kernel, not a measurement" if args.cpu_dry_run else
+                 "synthetic (SURVEY 8(d) start states, u_RL ~ U[-1,1], "
+                 + ("prior mean/sigma" if args.prior == "prior" else "per-env mean/sigma tensors (post-GP-fit regime)")
+                 + ", seeded auto-resets)"),
+        "config": {"workload": f"{args.env} fused safe step (rcbf_safe_step), non-diff CBF-QP, {hz}"
+                               f"batch {B} envs per GPU, {args.solver} fp64 QP, {launch}",
+                   "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
+                   "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)",
+                   "prior": args.prior, "qp_active_frac_at_start": round(active_frac, 4)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "kernel": "k_safe_step", "bytes_per_env_step": bps, "bytes_per_launch": B * bps,
+                     "kernel_ms": round(kern_ms, 5),
+                     "timing": "achieved = bytes_per_launch / kernel_ms; kernel_ms = HIP events around the timed "
+                               "region / steps (includes the graph launch and the inter-kernel gaps)"},
+    }
+    if extra:
+        rec["extra"] = extra
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.cpu_dry_run:
+        rec["cpu_baseline"] = cpu_baseline(args.env, args.hazards, args.cpu_seconds)
+        rec["cpu_reference_mode"] = cpu_reference_mode(args.env, args.hazards, args.cpu_seconds / 3)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def unicycle_hazards(k):
+    """The reference's hazard list (unicycle_env.py:25-26), first k."""
+    from rcbf_amd.envs import _EnvSpec
+    return _EnvSpec("Unicycle").hazards_locations[:k]
+
+
+def setup_gpu(args, dev, rank, B):
+    """Untimed set-up of the measured workload on this rank's GPU: envs at
+    SURVEY start states, the layer, a pool of u_RL batches, warm-up, and the
+    captured hipGraph (or the launch object of --launch seq / --no-graph)."""
+    from rcbf_amd import _lib, shard
     from rcbf_amd.diff_cbf_qp import CBFQPLayer
     from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
 
     class LArgs:
         cuda = True
 
-    B = args.batch
     solver = _lib.SOLVER_PDIPM if args.solver == "pdipm" else _lib.SOLVER_ACTIVE_SET
     if args.env == "SimulatedCars":
         env = BatchedSimulatedCarsEnv(B, device=dev, seed=1234, env_offset=shard.env_offset(rank, B))
     else:
-        from oracle.oracle import UNI  # constants only
         env = BatchedUnicycleEnv(B, device=dev, seed=1234, env_offset=shard.env_offset(rank, B),
-                                 hazards_locations=UNI["hazards"][:args.hazards])
+                                 hazards_locations=unicycle_hazards(args.hazards))
     layer = CBFQPLayer(env, LArgs(), gamma_b=20.0, solver=solver)
     S = args.steps if args.launch == "seq" else largest_divisor_le(args.steps, args.graph_steps)
     gen = torch.Generator(device=dev)
@@ -214,16 +369,20 @@ def main():
     init_states(env, gen, args.env)
     # 50 distinct u_RL batches, cycled through by the captured steps
     pool = [(torch.rand(B, env.n_u, device=dev, generator=gen) * 2 - 1).contiguous() for _ in range(min(S, 50))]
+    mean = sigma = None
+    if args.prior == "tensor":  # a fitted GP's per-env posterior (dynamics.py:342-390): small mean, sigma near MAX_STD
+        mean = (0.01 * torch.randn(B, env.n_s, device=dev, generator=gen)).contiguous()
+        sigma = (0.2 * torch.rand(B, env.n_s, device=dev, generator=gen) + 0.05).contiguous()
     outs = env.make_outputs()
     if args.env == "SimulatedCars":
         outs["goal_met"] = None
 
     def steps(n, off=0):
         for j in range(n):
-            env.safe_step(pool[(off + j) % len(pool)], layer, outputs=outs)
+            env.safe_step(pool[(off + j) % len(pool)], layer, mean=mean, sigma=sigma, outputs=outs)
 
     # fraction of envs whose safety filter changes the action at the start states
-    env.safe_step(pool[0], layer, outputs=outs)
+    steps(1)
     active_frac = float((outs["u"] != pool[0]).any(1).float().mean().item())
     # warmup (eager), then capture S fused steps into one hipGraph
     steps(max(args.warmup, 1))
@@ -231,7 +390,7 @@ def main():
     if args.launch == "seq" and not args.no_graph:
         class _Seq:
             def replay(self):
-                env.safe_step_seq(pool, layer, outputs=outs, steps=S)
+                env.safe_step_seq(pool, layer, mean=mean, sigma=sigma, outputs=outs, steps=S)
         graph = _Seq()
         graph.replay()
     elif args.no_graph:
@@ -252,65 +411,7 @@ def main():
             graph.replay()
     torch.cuda.synchronize()
     env.check_failures()
-
-    reps = args.steps // S
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    shard.barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(reps):
-        graph.replay()
-    ev1.record()
-    torch.cuda.synchronize()
-    shard.barrier(world)
-    el = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # per fused-step launch, on the launch stream
-    env.check_failures()
-    el = shard.max_over_ranks(el, world, dev)
-    kern_ms = shard.max_over_ranks(kern_ms, world, dev)
-    value = shard.whole_job_rate(world, B, args.steps, el)
-    bps = BYTES_PER_STEP[args.env]
-    achieved = B * bps / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.env, B)
-    extra = {}
-    if args.extra and rank == 0:
-        extra = extra_measurements(env, layer, dev, args)
-    rec = {
-        "metric": "safe env steps/sec (dynamics+CBF-QP) at batch 65536, 1/2/4/8 MI355X",
-        "value": round(value, 1),
-        "unit": "safe env steps/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(el / args.steps * 1e3, 5),
-        "higher_is_better": True,
-        "scaling": args.scaling,
-        "vs_baseline": None,
-        "dtype": "f32 rows / f64 QP / f64 env",
-        "data": "synthetic (SURVEY 8(d) start states, u_RL ~ U[-1,1], prior mean/sigma, seeded auto-resets)",
-        "config": {"workload": f"{args.env} fused safe step (rcbf_safe_step), non-diff CBF-QP, "
-                               f"{'3-hazard ' if args.env == 'Unicycle' and args.hazards == 3 else ''}"
-                               f"batch {B} envs per GPU, {args.solver} fp64 QP, "
-                               f"{'eager launches' if args.no_graph else f'hipGraph of {S} steps'}",
-                   "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
-                   "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)",
-                   "qp_active_frac_at_start": round(active_frac, 4)},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "kernel": "k_safe_step", "bytes_per_launch": B * bps,
-                     "kernel_ms": round(kern_ms, 5)},
-    }
-    if extra:
-        rec["extra"] = extra
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline(args.env, args.hazards, args.cpu_seconds)
-        rec["cpu_reference_mode"] = cpu_reference_mode(args.env, args.hazards, args.cpu_seconds / 3)
-    if rank == 0:
-        print(json.dumps(rec), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    return env, layer, graph, S, active_frac
 
 
 def sac_update_safe_action(env, layer, dev):

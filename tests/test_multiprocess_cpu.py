@@ -84,3 +84,24 @@ def test_two_rank_gloo_shards_reproduce_unsharded_run():
     assert np.array_equal(x_sharded, x_full)
     assert el == 1.5  # max over ranks
     assert rate == pytest.approx(2 * (B_TOTAL // 2) * STEPS / 1.5)
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus 2` (no torchrun) starts 2 rank processes before
+    any GPU call; they rendezvous on 127.0.0.1, run the barrier / max-over-
+    ranks timing and rank 0 prints ONE JSON line for the whole job.  Here on
+    the CPU with gloo and no kernel (--cpu-dry-run)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--cpu-dry-run",
+                        "--steps", "5", "--warmup", "1", "--batch", "1024"],
+                       capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 2 * 1024
+    assert rec["config"]["parallelism"] == "env-shard x2 (no collective)" and rec["steps"] == 5
+    assert rec["value"] > 0 and "dry run" in rec["data"]
