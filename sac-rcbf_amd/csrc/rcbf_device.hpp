@@ -1081,6 +1081,19 @@ __device__ __forceinline__ void cars_qp_1d(const PMat<2, true>& pm, const R (*G)
 // As for cars, eps*(u) = max(0, max_j e_j(u)) with affine e_j(u) = a_j.u + b_j,
 // leaving the 2-D convex piecewise quadratic
 //   phi(u) = p0 u0^2 + p1 u1^2 + p2 eps*(u)^2   over the box.
+//
+// Pruning (exact): a hazard row whose e_j(u) <= 0 over the WHOLE box never
+// changes eps*(u) on the box -- phi on the box, hence the constrained optimum,
+// is the same with or without it.  Each lane keeps only its live rows
+// (max over the box of a_j.u + b_j > 0, i.e. the hazard can bind), compacted
+// into slots; the wave then solves with KK = the largest live count of its
+// lanes (a wave-uniform branch), so a lane far from every hazard costs one
+// clamp and a typical wave (<= 2 hazards within reach of any of its envs)
+// enumerates 2 pieces + 1 kink instead of K + K(K-1)/2 + C(K,3) candidates.
+// Unused slots of a lane repeat its first slot (a duplicated piece only adds
+// NaN kink / triple candidates, which never win, and duplicate points).
+//
+// uni_pieces_solve<KK> on the slots:
 // Stage 1, box-free optimum: it is u = 0, the stationary point of one piece
 // (Sherman-Morrison on diag(p0,p1) + p2 a a'), the minimiser on one kink line
 // e_i = e_j, or a triple point e_i = e_j = e_l (phi is differentiable where an
@@ -1092,7 +1105,125 @@ __device__ __forceinline__ void cars_qp_1d(const PMat<2, true>& pm, const R (*G)
 // 1-D problem solved exactly like cars_qp_1d (clamped stationary points and
 // kinks).  For a coordinate u_f does not violate, the "edge" is an interior
 // line whose candidates are still feasible points -- harmless -- so both
-// edges run branch-free in every lane.
+// edges run branch-free in every lane.  (Stage 2 stays exact for the pruned
+// phi: it equals the full phi on the box, and the facing-edge argument holds
+// for any convex function.)
+template <int KK>
+__device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2, double ip0, double ip1,
+                                                 const double* a0, const double* a1, const double* b, double L0,
+                                                 double U0, double L1, double U1, double& bu0, double& bu1,
+                                                 double& bf) {
+    auto eps_of = [&](double u0, double u1) {
+        double e = 0.0;
+#pragma unroll
+        for (int j = 0; j < KK; ++j) e = fmax(e, fma(a0[j], u0, fma(a1[j], u1, b[j])));
+        return e;
+    };
+    auto phi = [&](double u0, double u1) {
+        double e = eps_of(u0, u1);
+        return fma(p0 * u0, u0, fma(p1 * u1, u1, p2 * e * e));
+    };
+    bu0 = 0.0;
+    bu1 = 0.0;
+    bf = phi(0.0, 0.0);
+    auto take = [&](double u0, double u1) {
+        double f = phi(u0, u1);
+        bool t = f < bf;  // NaN candidates never win
+        bu0 = t ? u0 : bu0;
+        bu1 = t ? u1 : bu1;
+        bf = fmin(bf, f);  // = t ? f : bf (fmin drops a NaN f)
+    };
+    // stage 1: box-free candidates
+#pragma unroll
+    for (int j = 0; j < KK; ++j) {  // piece j: (diag(p0,p1) + p2 a a') u = -p2 b a
+        double w0 = a0[j] * ip0, w1 = a1[j] * ip1;
+        double sden = fma(p2, fma(a0[j], w0, a1[j] * w1), 1.0);
+        double f = -p2 * b[j] * rcp64_qp_nz(sden);
+        take(f * w0, f * w1);
+    }
+#pragma unroll
+    for (int i = 0; i < KK; ++i) {
+#pragma unroll
+        for (int j = i + 1; j < KK; ++j) {  // kink line (a_i - a_j).u = b_j - b_i, minimise along it
+            double d0 = a0[i] - a0[j], d1 = a1[i] - a1[j], c = b[j] - b[i];
+            // parallel pieces (dd = 0) give NaN through rcp64_qp_nz and never win
+            double dd = fma(d0, d0, d1 * d1);
+            double idd = rcp64_qp_nz(dd);
+            double q0 = c * d0 * idd, q1 = c * d1 * idd;  // a point on the line
+            double n0 = -d1, n1 = d0;                     // its direction
+            double ea = fma(a0[i], q0, fma(a1[i], q1, b[i])), an = fma(a0[i], n0, a1[i] * n1);
+            double num = fma(p0 * q0, n0, fma(p1 * q1, n1, p2 * ea * an));
+            double den = fma(p0 * n0, n0, fma(p1 * n1, n1, p2 * an * an));
+            double t = -num * rcp64_qp_nz(den);
+            take(fma(t, n0, q0), fma(t, n1, q1));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < KK; ++i) {
+#pragma unroll
+        for (int j = i + 1; j < KK; ++j) {
+#pragma unroll
+            for (int l = j + 1; l < KK; ++l) {  // triple point e_i = e_j = e_l
+                double m00 = a0[i] - a0[j], m01 = a1[i] - a1[j], r0 = b[j] - b[i];
+                double m10 = a0[i] - a0[l], m11 = a1[i] - a1[l], r1 = b[l] - b[i];
+                double det = fma(m00, m11, -m01 * m10);
+                double id = rcp64_qp_nz(det);  // det = 0: NaN, never wins
+                take((r0 * m11 - r1 * m01) * id, (m00 * r1 - m10 * r0) * id);
+            }
+        }
+    }
+    const bool inbox = (bu0 >= L0) && (bu0 <= U0) && (bu1 >= L1) && (bu1 <= U1);
+    // stage 2 (branch-free): the facing u0-edge and u1-edge
+    const double v0 = fmin(fmax(bu0, L0), U0), v1 = fmin(fmax(bu1, L1), U1);
+    bf = inbox ? bf : __builtin_huge_val();  // an out-of-box stage-1 point must not win
+    auto edge = [&](bool fix0, double v, double lo, double hi) {
+        // free coordinate y in [lo, hi]; e_j = al_j y + be_j and
+        // phi(y) = pf y^2 + (p_fixed v^2 + p2 eps(y)^2)
+        double al[KK], be[KK];
+#pragma unroll
+        for (int j = 0; j < KK; ++j) {
+            al[j] = fix0 ? a1[j] : a0[j];
+            be[j] = fix0 ? fma(a0[j], v, b[j]) : fma(a1[j], v, b[j]);
+        }
+        const double pf = fix0 ? p1 : p0;
+        const double cfix = (fix0 ? p0 : p1) * v * v;
+        auto cand = [&](double y) {
+            y = fmin(fmax(y, lo), hi);
+            double e = 0.0;
+#pragma unroll
+            for (int j = 0; j < KK; ++j) e = fmax(e, fma(al[j], y, be[j]));
+            const double f = fma(pf * y, y, fma(p2 * e, e, cfix));
+            const bool t = f < bf;
+            bu0 = t ? (fix0 ? v : y) : bu0;
+            bu1 = t ? (fix0 ? y : v) : bu1;
+            bf = fmin(bf, f);
+        };
+        cand(0.0);
+#pragma unroll
+        for (int j = 0; j < KK; ++j) cand(-(p2 * al[j] * be[j]) * rcp64_qp_nz(fma(p2 * al[j], al[j], pf)));
+#pragma unroll
+        for (int i = 0; i < KK; ++i)
+#pragma unroll
+            for (int j = i + 1; j < KK; ++j) {
+                // den = 0: NaN, which the clamp in cand turns into the feasible point lo
+                double den = al[i] - al[j];
+                cand((be[j] - be[i]) * rcp64_qp_nz(den));
+            }
+    };
+    edge(true, v0, L1, U1);
+    edge(false, v1, L0, U0);
+}
+
+// Wave-uniform maximum of a small per-lane count (0..K).
+template <int K>
+__device__ __forceinline__ int wave_max_count(int cnt) {
+    int kmax = 0;
+#pragma unroll
+    for (int t = 1; t <= K; ++t)
+        if (__ballot(cnt >= t) != 0) kmax = t;
+    return kmax;
+}
+
 template <int K, typename R>
 __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[3], const R* h, double* z,
                                           int& status) {
@@ -1112,108 +1243,55 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
     const double L0 = (double)h[K + 1] * rcp64_qp_nz((double)G[K + 1][0]);
     const double U1 = (double)h[K + 2] * rcp64_qp_nz((double)G[K + 2][1]);
     const double L1 = (double)h[K + 3] * rcp64_qp_nz((double)G[K + 3][1]);
-    auto eps_of = [&](double u0, double u1) {
-        double e = 0.0;
+    // live rows: max over the box of e_j(u) > 0 (NaN data keeps the row; such a lane fails below anyway)
+    double A0[K], A1[K], Bv[K];
+    int cnt = 0;
 #pragma unroll
-        for (int j = 0; j < K; ++j) e = fmax(e, fma(a0[j], u0, fma(a1[j], u1, b[j])));
-        return e;
-    };
-    auto phi = [&](double u0, double u1) {
-        double e = eps_of(u0, u1);
-        return fma(p0 * u0, u0, fma(p1 * u1, u1, p2 * e * e));
-    };
-    double bu0 = 0.0, bu1 = 0.0, bf = phi(0.0, 0.0);
-    auto take = [&](double u0, double u1) {
-        double f = phi(u0, u1);
-        bool t = f < bf;  // NaN candidates never win
-        bu0 = t ? u0 : bu0;
-        bu1 = t ? u1 : bu1;
-        bf = fmin(bf, f);  // = t ? f : bf (fmin drops a NaN f)
-    };
-    // stage 1: box-free candidates
-#pragma unroll
-    for (int j = 0; j < K; ++j) {  // piece j: (diag(p0,p1) + p2 a a') u = -p2 b a
-        double w0 = a0[j] * ip0, w1 = a1[j] * ip1;
-        double sden = fma(p2, fma(a0[j], w0, a1[j] * w1), 1.0);
-        double f = -p2 * b[j] * rcp64_qp_nz(sden);
-        take(f * w0, f * w1);
+    for (int s = 0; s < K; ++s) {
+        A0[s] = a0[0];
+        A1[s] = a1[0];
+        Bv[s] = b[0];
     }
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
+    for (int j = 0; j < K; ++j) {
+        const double emax = b[j] + fmax(a0[j] * L0, a0[j] * U0) + fmax(a1[j] * L1, a1[j] * U1);
+        const bool live = !(emax <= 0.0);
 #pragma unroll
-        for (int j = i + 1; j < K; ++j) {  // kink line (a_i - a_j).u = b_j - b_i, minimise along it
-            double d0 = a0[i] - a0[j], d1 = a1[i] - a1[j], c = b[j] - b[i];
-            // parallel pieces (dd = 0) give NaN through rcp64_qp_nz and never win
-            double dd = fma(d0, d0, d1 * d1);
-            double idd = rcp64_qp_nz(dd);
-            double q0 = c * d0 * idd, q1 = c * d1 * idd;  // a point on the line
-            double n0 = -d1, n1 = d0;                     // its direction
-            double ea = fma(a0[i], q0, fma(a1[i], q1, b[i])), an = fma(a0[i], n0, a1[i] * n1);
-            double num = fma(p0 * q0, n0, fma(p1 * q1, n1, p2 * ea * an));
-            double den = fma(p0 * n0, n0, fma(p1 * n1, n1, p2 * an * an));
-            double t = -num * rcp64_qp_nz(den);
-            take(fma(t, n0, q0), fma(t, n1, q1));
+        for (int s = 0; s <= j; ++s) {  // row j can only land in slots 0..j
+            const bool here = live && (cnt == s);
+            A0[s] = here ? a0[j] : A0[s];
+            A1[s] = here ? a1[j] : A1[s];
+            Bv[s] = here ? b[j] : Bv[s];
         }
+        cnt += live ? 1 : 0;
     }
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-#pragma unroll
-        for (int j = i + 1; j < K; ++j) {
-#pragma unroll
-            for (int l = j + 1; l < K; ++l) {  // triple point e_i = e_j = e_l
-                double m00 = a0[i] - a0[j], m01 = a1[i] - a1[j], r0 = b[j] - b[i];
-                double m10 = a0[i] - a0[l], m11 = a1[i] - a1[l], r1 = b[l] - b[i];
-                double det = fma(m00, m11, -m01 * m10);
-                double id = rcp64_qp_nz(det);  // det = 0: NaN, never wins
-                take((r0 * m11 - r1 * m01) * id, (m00 * r1 - m10 * r0) * id);
-            }
-        }
+    for (int s = 1; s < K; ++s) {  // unused slots repeat slot 0
+        A0[s] = (s < cnt) ? A0[s] : A0[0];
+        A1[s] = (s < cnt) ? A1[s] : A1[0];
+        Bv[s] = (s < cnt) ? Bv[s] : Bv[0];
     }
-    const bool inbox = (bu0 >= L0) && (bu0 <= U0) && (bu1 >= L1) && (bu1 <= U1);
-    {
-        // stage 2 (branch-free): the facing u0-edge and u1-edge
-        const double v0 = fmin(fmax(bu0, L0), U0), v1 = fmin(fmax(bu1, L1), U1);
-        bf = inbox ? bf : __builtin_huge_val();  // an out-of-box stage-1 point must not win
-        auto edge = [&](bool fix0, double v, double lo, double hi) {
-            // free coordinate y in [lo, hi]; e_j = al_j y + be_j and
-            // phi(y) = pf y^2 + (p_fixed v^2 + p2 eps(y)^2)
-            double al[K], be[K];
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                al[j] = fix0 ? a1[j] : a0[j];
-                be[j] = fix0 ? fma(a0[j], v, b[j]) : fma(a1[j], v, b[j]);
-            }
-            const double pf = fix0 ? p1 : p0;
-            const double cfix = (fix0 ? p0 : p1) * v * v;
-            auto cand = [&](double y) {
-                y = fmin(fmax(y, lo), hi);
-                double e = 0.0;
-#pragma unroll
-                for (int j = 0; j < K; ++j) e = fmax(e, fma(al[j], y, be[j]));
-                const double f = fma(pf * y, y, fma(p2 * e, e, cfix));
-                const bool t = f < bf;
-                bu0 = t ? (fix0 ? v : y) : bu0;
-                bu1 = t ? (fix0 ? y : v) : bu1;
-                bf = fmin(bf, f);
-            };
-            cand(0.0);
-#pragma unroll
-            for (int j = 0; j < K; ++j) cand(-(p2 * al[j] * be[j]) * rcp64_qp_nz(fma(p2 * al[j], al[j], pf)));
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-#pragma unroll
-                for (int j = i + 1; j < K; ++j) {
-                    // den = 0: NaN, which the clamp in cand turns into the feasible point lo
-                    double den = al[i] - al[j];
-                    cand((be[j] - be[i]) * rcp64_qp_nz(den));
-                }
-        };
-        edge(true, v0, L1, U1);
-        edge(false, v1, L0, U0);
+    double bu0, bu1, bf;
+    const int kmax = wave_max_count<K>(cnt);
+    if (kmax == 0) {  // no hazard row can bind anywhere in the box, for every lane of the wave
+        bu0 = fmin(fmax(0.0, L0), U0);
+        bu1 = fmin(fmax(0.0, L1), U1);
+        bf = 0.0;
+    } else if (kmax == 1 || K == 1) {
+        uni_pieces_solve<1>(p0, p1, p2, ip0, ip1, A0, A1, Bv, L0, U0, L1, U1, bu0, bu1, bf);
+    } else if (kmax == 2 || K == 2) {
+        uni_pieces_solve<(K >= 2 ? 2 : 1)>(p0, p1, p2, ip0, ip1, A0, A1, Bv, L0, U0, L1, U1, bu0, bu1, bf);
+    } else if (kmax == 3 || K == 3) {
+        uni_pieces_solve<(K >= 3 ? 3 : 1)>(p0, p1, p2, ip0, ip1, A0, A1, Bv, L0, U0, L1, U1, bu0, bu1, bf);
+    } else {
+        uni_pieces_solve<K>(p0, p1, p2, ip0, ip1, A0, A1, Bv, L0, U0, L1, U1, bu0, bu1, bf);
     }
     z[0] = bu0;
     z[1] = bu1;
-    z[2] = eps_of(bu0, bu1);
+    double e = 0.0;  // eps at the optimum over ALL rows (the dropped ones are <= 0 there)
+#pragma unroll
+    for (int j = 0; j < K; ++j) e = fmax(e, fma(a0[j], bu0, fma(a1[j], bu1, b[j])));
+    z[2] = e;
     finite = finite && isfinite(U0 + L0 + U1 + L1);  // fmin/fmax would hide a NaN bound
     const bool ok = isfinite(z[0]) && isfinite(z[1]) && isfinite(z[2]) && bf < __builtin_huge_val();
     status = !finite ? RCBF_QP_NONFINITE : (ok && L0 <= U0 && L1 <= U1 ? RCBF_QP_OK : RCBF_QP_INFEASIBLE);

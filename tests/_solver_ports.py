@@ -51,17 +51,15 @@ def cars_qp_1d(Gn, hn, pd):
     return np.stack([u, eps(u)], 1)
 
 
-def uni_qp_2d(Gn, hn, pd, K):
+def uni_qp_2d(Gn, hn, pd, K, prune=True, wave=64):
     """Unicycle QP: variables (u0, u1, eps), rows [K cbf rows, 4 box rows].
-    Stage 1: box-free minimisers (origin, per-piece Sherman-Morrison
-    stationary points, minimisers on each kink line, triple points); the best
-    one is the unconstrained optimum of phi.  If it lies outside the box, the
-    constrained optimum lies on a facing edge (u0 or u1 fixed to its clamped
-    value); each edge is a 1-D problem solved like cars_qp_1d.
-    Returns ((B,3) z, in-box mask)."""
+    Pruning (as the kernel): per lane, only the rows whose a_j.u + b_j can
+    exceed 0 somewhere in the box are kept, compacted into slots (unused
+    slots repeat slot 0); lanes are grouped in waves of `wave` and each wave
+    solves with KK = its largest live count (KK = 0: the clamped origin).
+    Returns ((B,3) z, in-box mask of the stage-1 point, KK per lane)."""
     G = Gn.astype(np.float64)
     h = hn.astype(np.float64)
-    p0, p1, p2 = pd
     B = G.shape[0]
     inv = 1 / G[:, :K, 2]
     a0 = -G[:, :K, 0] * inv
@@ -71,6 +69,49 @@ def uni_qp_2d(Gn, hn, pd, K):
     L0 = h[:, K + 1] / G[:, K + 1, 0]
     U1 = h[:, K + 2] / G[:, K + 2, 1]
     L1 = h[:, K + 3] / G[:, K + 3, 1]
+    if not prune:
+        z, inb = _pieces_solve(a0, a1, b, L0, U0, L1, U1, pd)
+        return _with_eps(z, a0, a1, b), inb, np.full(B, K)
+    emax = b + np.maximum(a0 * L0[:, None], a0 * U0[:, None]) + np.maximum(a1 * L1[:, None], a1 * U1[:, None])
+    live = ~(emax <= 0)
+    cnt = live.sum(1)
+    A0, A1, Bv = (np.repeat(v[:, :1], K, 1) for v in (a0, a1, b))
+    pos = np.cumsum(live, 1) - 1
+    for j in range(K):
+        sel = live[:, j]
+        r = np.nonzero(sel)[0]
+        A0[r, pos[r, j]], A1[r, pos[r, j]], Bv[r, pos[r, j]] = a0[r, j], a1[r, j], b[r, j]
+    for sl in range(1, K):
+        unused = sl >= cnt
+        A0[unused, sl], A1[unused, sl], Bv[unused, sl] = A0[unused, 0], A1[unused, 0], Bv[unused, 0]
+    nw = (B + wave - 1) // wave
+    kk = np.zeros(nw * wave, int)
+    kk[:B] = cnt
+    kk = np.repeat(kk.reshape(nw, wave).max(1), wave)[:B]
+    z = np.zeros((B, 2))
+    inb = np.ones(B, bool)
+    for KK in range(K + 1):
+        r = np.nonzero(kk == KK)[0]
+        if r.size == 0:
+            continue
+        if KK == 0:
+            z[r, 0] = np.minimum(np.maximum(0.0, L0[r]), U0[r])
+            z[r, 1] = np.minimum(np.maximum(0.0, L1[r]), U1[r])
+            continue
+        zr, ir = _pieces_solve(A0[r, :KK], A1[r, :KK], Bv[r, :KK], L0[r], U0[r], L1[r], U1[r], pd)
+        z[r], inb[r] = zr, ir
+    return _with_eps(z, a0, a1, b), inb, kk
+
+
+def _with_eps(z, a0, a1, b):
+    e = np.maximum(0, (a0 * z[:, :1] + a1 * z[:, 1:2] + b).max(1))
+    return np.concatenate([z, e[:, None]], 1)
+
+
+def _pieces_solve(a0, a1, b, L0, U0, L1, U1, pd):
+    """Stage 1 + stage 2 of the kernel's uni_pieces_solve on K pieces."""
+    p0, p1, p2 = pd
+    B, K = a0.shape
 
     def eps(u0, u1):
         return np.maximum(0, (a0 * u0[:, None] + a1 * u1[:, None] + b).max(1))
@@ -140,4 +181,4 @@ def uni_qp_2d(Gn, hn, pd, K):
             best = np.where(t, f, best)
             bu0 = np.where(t, u0, bu0)
             bu1 = np.where(t, u1, bu1)
-    return np.stack([bu0, bu1, eps(bu0, bu1)], 1), inb
+    return np.stack([bu0, bu1], 1), inb

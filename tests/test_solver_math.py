@@ -77,11 +77,14 @@ def test_uni_qp_2d_matches_enumeration(K, gamma):
     Gn, hn, _ = O.normalize_rows(G, h)
     pd = np.array([np.float64(F(1.0)), np.float64(F(1e-2)), np.float64(F(1e5))])
     z, lam, act, st = O.qp_exact(pd, Gn, hn)
-    z2, inb = uni_qp_2d(Gn, hn, pd, K)
+    z2, inb, kk = uni_qp_2d(Gn, hn, pd, K)
+    z3, _, _ = uni_qp_2d(Gn, hn, pd, K, prune=False)
     ok = st == 0
     assert ok.mean() > 0.999
     err = np.abs(z2 - z).max(1) / np.maximum(1, np.abs(z).max(1))
     assert err[ok].max() < 1e-6
+    assert np.abs(z3 - z)[ok].max() / max(1, np.abs(z[ok]).max()) < 1e-6
+    assert kk.min() < K  # pruning is exercised
     fin = np.clip(u + z[:, :2].astype(F), -2.5, 2.5)
     fin2 = np.clip(u + z2[:, :2].astype(F), -2.5, 2.5)
     assert (fin[ok] != fin2[ok]).any(1).mean() <= 1e-3
@@ -100,7 +103,29 @@ def test_uni_qp_2d_cascade(K):
     Gn, hn, _ = O.normalize_rows(G, h)
     pd = np.array([10.0, 1e-4, 1e7])
     z, lam, act, st = O.qp_exact(pd, Gn, hn)
-    z2, _ = uni_qp_2d(Gn, hn, pd, K)
+    z2, _, _ = uni_qp_2d(Gn, hn, pd, K)
     ok = st == 0
     err = np.abs(z2[:, :2] - z[:, :2]).max(1) / np.maximum(1, np.abs(z[:, :2]).max(1))
     assert err[ok].max() < 1e-6
+
+
+@pytest.mark.parametrize("K", [3, 5])
+def test_uni_pruning_on_the_bench_distribution(K):
+    """SURVEY 8(d) config-3 states (x, y ~ U[-3, 3], theta ~ U[-pi, pi]): the
+    pruned solver (waves of 64 lanes) equals the exhaustive enumeration, and
+    almost every wave needs at most 2 pieces (what makes the kernel cheap)."""
+    rng = np.random.default_rng(30 + K)
+    B = 64 * 600
+    hz = O.UNI["hazards"][:K]
+    x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1).astype(F)
+    u = rng.uniform(-1, 1, (B, 2)).astype(F)
+    P, q, G, h = O.unicycle_build_diff(x, u, np.zeros((B, 3), F), np.full((B, 3), 0.2, F), 20.0, hz)
+    Gn, hn, _ = O.normalize_rows(G, h)
+    pd = np.array([np.float64(F(1.0)), np.float64(F(1e-2)), np.float64(F(1e5))])
+    z, lam, act, st = O.qp_exact(pd, Gn, hn)
+    z2, _, kk = uni_qp_2d(Gn, hn, pd, K)
+    ok = st == 0
+    err = np.abs(z2 - z).max(1) / np.maximum(1, np.abs(z).max(1))
+    assert err[ok].max() < 1e-6
+    waves = kk[::64]
+    assert (waves <= 2).mean() > 0.9, np.bincount(waves)
