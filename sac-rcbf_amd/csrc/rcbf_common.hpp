@@ -225,14 +225,18 @@ __device__ __forceinline__ void cascade_P(double* d) {
     }
 }
 
+// cs_row [unicycle, nullable]: fp32 cos/sin of xs[2] already known (the fused step)
 template <int MODE, int K>
 __device__ __forceinline__ void diff_rows(const rcbf_params& prm, const float* xs, const float* u,
                                           const float* mu, const float* sig,
-                                          float (*G)[Dims<MODE, K>::N], float* h) {
+                                          float (*G)[Dims<MODE, K>::N], float* h, const float* cs_row = nullptr) {
     if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
         cars_rows_diff(prm, xs, u[0], sig[5], sig[7], sig[9], G, h);
     } else {
-        uni_rows_diff<K>(prm, xs, u, mu, sig, G, h);
+        if (cs_row)
+            uni_rows_diff_cs<K>(prm, xs, cs_row[0], cs_row[1], u, mu, sig, G, h);
+        else
+            uni_rows_diff<K>(prm, xs, u, mu, sig, G, h);
     }
 }
 
@@ -256,7 +260,8 @@ struct LayerState {
 template <int SOLVER, int MODE, int K, bool NEED_LAM = false>
 __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const float* xs, const float* u,
                                               const float* mu, const float* sig, float* u_final,
-                                              LayerState<MODE, K>& L, unsigned long long* stamps = nullptr) {
+                                              LayerState<MODE, K>& L, unsigned long long* stamps = nullptr,
+                                              const float* cs_row = nullptr) {
     using D = Dims<MODE, K>;
     if constexpr ((kAblate & 2) != 0) {
 #pragma unroll
@@ -264,7 +269,7 @@ __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const floa
         L.qp.status = RCBF_QP_OK;
         return;
     }
-    diff_rows<MODE, K>(prm, xs, u, mu, sig, L.G, L.h);
+    diff_rows<MODE, K>(prm, xs, u, mu, sig, L.G, L.h, cs_row);
 #pragma unroll
     for (int r = 0; r < D::M; ++r) {
         L.hraw[r] = L.h[r];
@@ -352,11 +357,7 @@ __device__ __forceinline__ void state_from_obs32(const float* o, float* s32) {
     } else {
         s32[0] = o[0];
         s32[1] = o[1];
-#ifdef RCBF_STUDY_NO_ATAN2  // performance study only: what the atan2 costs (wrong state)
-        s32[2] = o[3] + o[2];
-#else
         s32[2] = (float)atan2((double)o[3], (double)o[2]);
-#endif
     }
 }
 
@@ -385,10 +386,18 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
                                               float* u_out = nullptr, bool ep_pre = false, uint32_t ep0 = 0) {
     using D = Dims<MODE, K>;
     float s32[D::NS];
-    state_from_env<MODE>(xs, s32);
+    float cs_row[2];
+    double c_th = 0.0, s_th = 0.0;  // unicycle: cos/sin of the pre-step theta, shared by obs, rows and env step
+    if constexpr (MODE == RCBF_MODE_UNICYCLE) {
+        sincos(xs[2], &s_th, &c_th);
+        uni_state32_from_cs(xs, c_th, s_th, s32, cs_row[0], cs_row[1]);
+    } else {
+        state_from_env<MODE>(xs, s32);
+    }
     RCBF_STAMP(stamps, 2, false);
     LayerState<MODE, K> L;
-    layer_forward<SOLVER, MODE, K>(prm, s32, us, m, s, uf, L, stamps);
+    layer_forward<SOLVER, MODE, K>(prm, s32, us, m, s, uf, L, stamps,
+                                   MODE == RCBF_MODE_UNICYCLE ? cs_row : nullptr);
     status = L.qp.status;
     // issue the safe-action store now so its write overlaps the env step
     if (u_out) {
@@ -419,7 +428,7 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
         gm = false;
     } else {
         UniStepOut o;
-        uni_env_step<float>(prm, xs, a, st, uf, o);
+        uni_env_step_cs<float>(prm, xs, a, st, uf, c_th, s_th, o);
         rew = (float)o.reward;
         cst = (float)o.cost;
         dn = o.done;

@@ -1447,22 +1447,13 @@ __device__ __forceinline__ void cars_rows_cascade(const rcbf_params& prm, const 
 
 // Unicycle, CBFQPLayer form (diff_cbf_qp.py:202-266, actuators 362-377), fp32.
 // K hazards -> rows 0..K-1; actuator rows K..K+3 in the reference's order.
+// rows from c = fp32 cos(theta32), s = fp32 sin(theta32) (theta32 = xs[2])
 template <int K>
-__device__ __forceinline__ void uni_rows_diff(const rcbf_params& prm, const float* xs, const float* u,
-                                              const float* mu, const float* sig, float (*G)[3],
-                                              float* h) {
+__device__ __forceinline__ void uni_rows_diff_cs(const rcbf_params& prm, const float* xs, float c, float s,
+                                                 const float* u, const float* mu, const float* sig,
+                                                 float (*G)[3], float* h) {
 #pragma clang fp contract(off)
     const float lp = (float)prm.l_p, g = (float)prm.gamma_b;
-    // fp32 cos/sin, correctly rounded from fp64 (torch's SLEEF is within 1 ulp)
-    double sd, cd;
-#ifdef RCBF_STUDY_NO_ROW_SINCOS  // performance study only: what the row sincos costs (wrong rows)
-    sd = (double)xs[2];
-    cd = 1.0 - 0.5 * sd * sd;
-#else
-    sincos((double)xs[2], &sd, &cd);  // one shared range reduction
-#endif
-    float c = (float)cd;
-    float s = (float)sd;
     float px = xs[0] + lp * c, py = xs[1] + lp * s;
     float g00 = c, g01 = -s * lp, g10 = s, g11 = c * lp;
     float mupx = g01 * mu[2] + mu[0], mupy = g11 * mu[2] + mu[1];
@@ -1494,6 +1485,57 @@ __device__ __forceinline__ void uni_rows_diff(const rcbf_params& prm, const floa
         h[r0] = (float)prm.u_max[c2] - u[c2];
         h[r0 + 1] = -(float)prm.u_min[c2] + u[c2];
     }
+}
+
+template <int K>
+__device__ __forceinline__ void uni_rows_diff(const rcbf_params& prm, const float* xs, const float* u,
+                                              const float* mu, const float* sig, float (*G)[3], float* h) {
+    // fp32 cos/sin, correctly rounded from fp64 (torch's SLEEF is within 1 ulp)
+    double sd, cd;
+    sincos((double)xs[2], &sd, &cd);  // one shared range reduction
+    uni_rows_diff_cs<K>(prm, xs, (float)cd, (float)sd, u, mu, sig, G, h);
+}
+
+// get_state(float(obs(x))) of a unicycle state whose cos/sin c, s (fp64) are
+// already known, plus the fp32 cos/sin of the resulting theta32 that the rows
+// need -- without the atan2 and the second sincos.
+//   obs[2:4] = (c32, s32) = RN32(c, s);  the reference's theta32 =
+//   RN32(atan2(s32, c32)) (dynamics.py:205-232, fp64 arctan2 then fp32).
+//   With ds = s32 - s, dc = c32 - c (exact, Sterbenz): atan2(s32, c32) =
+//   t + (c ds - s dc) / (c^2 + s^2) + O(|d|^2 ~ 4e-15), t = theta reduced to
+//   (-pi, pi] (two-constant Cody-Waite), wrapped to the side atan2 returns
+//   (the sign of s32).  Then cos/sin(theta32) = cos/sin(t + D) with
+//   D = theta32 - t' (|D| <~ 1e-7) by the addition formulas.  Both results
+//   are RN32 of a value within ~1e-15 of the exact one, i.e. the reference's
+//   value except within ~1e-15 of an fp32 rounding midpoint (a 1-ulp
+//   difference there; tests/test_solver_math.py test_uni_theta32_from_cos_sin).
+__device__ __forceinline__ void uni_state32_from_cs(const double* xs, double c, double s, float* s32, float& c_row,
+                                                    float& s_row) {
+    const double kPi = 3.141592653589793116, k2PiHi = 6.28318530717958623200, k2PiLo = 2.44929359829470635e-16;
+    const float c32 = (float)c, s32f = (float)s;
+    const double dc = (double)c32 - c, ds = (double)s32f - s;
+    const double k = rint(xs[2] * (1.0 / k2PiHi));
+    double t0 = fma(-k, k2PiLo, fma(-k, k2PiHi, xs[2]));  // the angle of (c, s), up to ~1e-16 k
+    const double den = fma(c, c, s * s);
+    double t = t0 + fma(c, ds, -s * dc) * rcp64_qp_nz(den);  // the angle of (c32, s32)
+    const double wrap = (s32f > 0.0f && t < 0.0) ? k2PiHi : ((s32f < 0.0f && t > 0.0) ? -k2PiHi : 0.0);
+    t += wrap;
+    t0 += wrap;
+    // exact zeros of s32: atan2(+-0, c32 > 0) = +-0, atan2(+-0, c32 < 0) = +-pi (then |s| < 1e-45:
+    // the true angle is that value)
+    const double tz = c32 < 0.0f ? __builtin_copysign(kPi, (double)s32f) : __builtin_copysign(0.0, (double)s32f);
+    t = (s32f == 0.0f) ? tz : t;
+    t0 = (s32f == 0.0f) ? tz : t0;
+    const float th32 = (float)t;
+    s32[0] = (float)xs[0];
+    s32[1] = (float)xs[1];
+    s32[2] = th32;
+    // cos/sin(theta32) = cos/sin(t0 + D) with (c, s) = cos/sin(t0), D = theta32 - t0 (|D| <~ 2e-7)
+    const double D = (double)th32 - t0;
+    const double D2 = D * D;
+    const double cD = fma(D2, fma(D2, 1.0 / 24.0, -0.5), 1.0), sD = D * fma(D2, -1.0 / 6.0, 1.0);
+    c_row = (float)fma(c, cD, -(s * sD));
+    s_row = (float)fma(s, cD, c * sD);
 }
 
 // Unicycle, CascadeCBFLayer form (cbf_qp.py:91-147), fp64: signed sigma_p,
@@ -1656,12 +1698,15 @@ __device__ __forceinline__ void uni_obs_cs(const double* xs, double c, double s,
     double v0 = r0 * c + r1 * s;
     double v1 = r0 * (-s) + r1 * c;
     double nrm = sqrt(v0 * v0 + v1 * v1) + 0.001;
+    // the fused step stores these as fp32: one reciprocal (within an ulp of
+    // the fp64 quotient, so the same fp32 value but at an fp32 rounding midpoint)
+    const double rn = rcp64_nz(nrm);
     o[0] = xs[0];
     o[1] = xs[1];
     o[2] = c;
     o[3] = s;
-    o[4] = v0 / nrm;
-    o[5] = v1 / nrm;
+    o[4] = v0 * rn;
+    o[5] = v1 * rn;
     o[6] = exp(-gd);
 }
 
@@ -1695,15 +1740,13 @@ struct UniStepOut {
 // safety filter, Euler step with g(x), then the -(dt*0.1) g(x') [cos th', 0]
 // drift evaluated left to right (:87).
 template <typename A>
-__device__ __forceinline__ void uni_env_step(const rcbf_params& prm, double* xs, double& last_dist, int& step,
-                                             const A* action, UniStepOut& o) {
+__device__ __forceinline__ void uni_env_step_cs(const rcbf_params& prm, double* xs, double& last_dist, int& step,
+                                                const A* action, double c, double s, UniStepOut& o) {
 #pragma clang fp contract(off)
     A a0c = action[0] < (A)(-1) ? (A)(-1) : (action[0] > (A)1 ? (A)1 : action[0]);
     A a1c = action[1] < (A)(-1) ? (A)(-1) : (action[1] > (A)1 ? (A)1 : action[1]);
     double a0 = (double)a0c, a1 = (double)a1c;
     const double dt = 0.02;
-    double c, s;
-    sincos(xs[2], &s, &c);
     // f = 0: 0.0 + g u equals g u up to the sign of a zero (skipped)
     xs[0] += dt * (c * a0);
     xs[1] += dt * (s * a0);
@@ -1734,6 +1777,14 @@ __device__ __forceinline__ void uni_env_step(const rcbf_params& prm, double* xs,
         hit = hit || (ex * ex + ey * ey < r2);
     }
     o.cost = hit ? 0.1 : 0.0;
+}
+
+template <typename A>
+__device__ __forceinline__ void uni_env_step(const rcbf_params& prm, double* xs, double& last_dist, int& step,
+                                             const A* action, UniStepOut& o) {
+    double c, s;
+    sincos(xs[2], &s, &c);
+    uni_env_step_cs<A>(prm, xs, last_dist, step, action, c, s, o);
 }
 
 // ---------------------------------------------------------------------------

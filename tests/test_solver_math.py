@@ -129,3 +129,51 @@ def test_uni_pruning_on_the_bench_distribution(K):
     assert err[ok].max() < 1e-6
     waves = kk[::64]
     assert (waves <= 2).mean() > 0.9, np.bincount(waves)
+
+
+def _fma(a, b, c):
+    """fma emulated in x87 extended precision (64-bit significand): within
+    an ulp of the fused result, enough for a statistics test."""
+    L = np.longdouble
+    return (L(a) * L(b) + L(c)).astype(np.float64)
+
+
+def test_uni_theta32_from_cos_sin():
+    """rcbf_device.hpp uni_state32_from_cs restated: theta32 and the rows'
+    fp32 cos/sin(theta32) from the fp64 cos/sin of the state's theta (no
+    atan2, no second sincos) equal the reference chain get_state(float(obs))
+    -> RN32(arctan2) -> RN32(cos/sin(theta32)) on >= 99.999 % of states and
+    are within 1 fp32 ulp on the rest; covers |theta| up to 200 rad, the
+    +-pi seam and multiples of pi/2."""
+    rng = np.random.default_rng(5)
+    th = np.concatenate([rng.uniform(-np.pi, np.pi, 200000), rng.uniform(-200, 200, 200000),
+                         np.pi + rng.normal(0, 1e-6, 20000), -np.pi + rng.normal(0, 1e-6, 20000),
+                         np.arange(-64, 65) * (np.pi / 2), [0.0, -0.0, np.pi, -np.pi]])
+    c, s = np.cos(th), np.sin(th)
+    c32, s32 = c.astype(F), s.astype(F)
+    ref_th = np.arctan2(s32.astype(np.float64), c32.astype(np.float64)).astype(F)
+    ref_c, ref_s = np.cos(ref_th.astype(np.float64)).astype(F), np.sin(ref_th.astype(np.float64)).astype(F)
+    hi, lo = 6.28318530717958623200, 2.44929359829470635e-16
+    k = np.rint(th * (1.0 / hi))
+    t0 = _fma(-k, lo, _fma(-k, hi, th))
+    dc, ds = c32.astype(np.float64) - c, s32.astype(np.float64) - s
+    t = t0 + _fma(c, ds, -s * dc) / _fma(c, c, s * s)
+    wrap = np.where((s32 > 0) & (t < 0), hi, np.where((s32 < 0) & (t > 0), -hi, 0.0))
+    t, t0 = t + wrap, t0 + wrap
+    tz = np.where(c32 < 0, np.copysign(np.pi, s32), np.copysign(0.0, s32))
+    t, t0 = np.where(s32 == 0, tz, t), np.where(s32 == 0, tz, t0)
+    th32 = t.astype(F)
+    D = th32.astype(np.float64) - t0
+    D2 = D * D
+    cD = _fma(D2, _fma(D2, 1.0 / 24.0, -0.5), 1.0)
+    sD = D * _fma(D2, -1.0 / 6.0, 1.0)
+    cr, sr = _fma(c, cD, -(s * sD)).astype(F), _fma(s, cD, c * sD).astype(F)
+    n_rand = 400000  # the random angles; the rest are seams and exact multiples of pi/2
+    for got, want in ((th32, ref_th), (cr, ref_c), (sr, ref_s)):
+        bad = got != want
+        assert bad[:n_rand].mean() < 1e-5, bad[:n_rand].mean()
+        # exact multiples of pi/2 of large magnitude: cos/sin ~ 4e-8 there, so the ~1e-16 absolute
+        # error of the reduction is ~2e-9 relative -- a 1-ulp fp32 difference on a few of them
+        assert bad.sum() <= 32
+        ulps = np.abs(got.view(np.int32).astype(np.int64) - want.view(np.int32).astype(np.int64))
+        assert ulps[bad].max(initial=0) <= 1
