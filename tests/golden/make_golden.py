@@ -266,7 +266,7 @@ def _layer_fixture(layer, x32, u32, mu32, sig32, w32):
                 final=final.detach().numpy(), grad_u=u.grad.numpy())
 
 
-def make_cars_layer(SimulatedCarsEnv, diff_cbf_qp, B=1024, seed=2, gamma_b=20.0):
+def make_cars_layer(SimulatedCarsEnv, diff_cbf_qp, B=4096, seed=2, gamma_b=20.0):
     rng = np.random.default_rng(seed)
     env = SimulatedCarsEnv()
     layer = _patch_layer(diff_cbf_qp.CBFQPLayer(env, _Args(), gamma_b=gamma_b, k_d=3.0, l_p=0.03))
@@ -294,7 +294,7 @@ def make_cars_layer(SimulatedCarsEnv, diff_cbf_qp, B=1024, seed=2, gamma_b=20.0)
     return out
 
 
-def make_unicycle_layer(UnicycleEnv, diff_cbf_qp, n_hazards, B=1024, seed=3, gamma_b=20.0, l_p=0.03):
+def make_unicycle_layer(UnicycleEnv, diff_cbf_qp, n_hazards, B=4096, seed=3, gamma_b=20.0, l_p=0.03):
     rng = np.random.default_rng(seed + n_hazards)
     env = UnicycleEnv()
     env.hazards_locations = env.hazards_locations[:n_hazards]
@@ -314,6 +314,94 @@ def make_unicycle_layer(UnicycleEnv, diff_cbf_qp, n_hazards, B=1024, seed=3, gam
     out["hazards"] = env.hazards_locations.astype(np.float64)
     out["gamma_b"] = np.float64(gamma_b)
     out["l_p"] = np.float64(l_p)
+    return out
+
+
+def make_f64_build(SimulatedCarsEnv, UnicycleEnv, diff_cbf_qp, B=4096, seed=17, gamma_b=20.0):
+    """SURVEY 8(c)(i) fp64 variant: the reference's CBFQPLayer with
+    torch.set_default_dtype(torch.float64) and fp64 inputs (the rows are then
+    built in fp64), on the config-2 / config-3 input distributions.  The HIP
+    layer builds rows in fp32 like the shipped reference; this fixture bounds
+    how far the fp32 build sits from an fp64 build (up to ~1e-4)."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        env = SimulatedCarsEnv()
+        layer = _patch_layer(diff_cbf_qp.CBFQPLayer(env, _Args(), gamma_b=gamma_b, k_d=3.0, l_p=0.03))
+        states, _ = _rollout_cars_states(SimulatedCarsEnv, B, rng)
+        x = states.astype(np.float32).astype(np.float64)  # the fp32 state the policy path hands over, widened
+        u = rng.uniform(-1, 1, size=(B, 1)).astype(np.float32).astype(np.float64)
+        mu = np.zeros((B, 10))
+        sig = np.tile(np.array([0, .2, 0, .2, 0, .2, 0, .2, 0, .2]), (B, 1))
+        w = rng.standard_normal((B, 1))
+        d = _layer_fixture(layer, x, u, mu, sig, w)
+        out.update({f"cars_{k}": v for k, v in d.items()})
+        for k in (3, 5):
+            env = UnicycleEnv()
+            env.hazards_locations = env.hazards_locations[:k]
+            layer = _patch_layer(diff_cbf_qp.CBFQPLayer(env, _Args(), gamma_b=gamma_b, k_d=1.5, l_p=0.03))
+            xs = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+            xs = xs.astype(np.float32).astype(np.float64)
+            uu = rng.uniform(-1, 1, size=(B, 2)).astype(np.float32).astype(np.float64)
+            d = _layer_fixture(layer, xs, uu, np.zeros((B, 3)), np.full((B, 3), 0.2), rng.standard_normal((B, 2)))
+            out.update({f"uni{k}_{kk}": v for kk, v in d.items()})
+            out[f"uni{k}_hazards"] = env.hazards_locations.astype(np.float64)
+    finally:
+        torch.set_default_dtype(old)
+    out["gamma_b"] = np.float64(gamma_b)
+    return out
+
+
+def make_sac_update(SimulatedCarsEnv, UnicycleEnv, diff_cbf_qp, dynamics, B=4096, seed=19, gamma_b=20.0):
+    """Config 5 (SimulatedCars batch 4096, diff CBF-QP forward + backward) as
+    the SAC update runs it: the reference's own RCBF_SAC.get_safe_action
+    (rcbf_sac/sac_cbf.py:218-238: DynamicsModel.get_state -> predict_disturbance
+    prior -> CBFQPLayer.get_safe_action) on an fp32 observation batch, then
+    d(sum(w * safe_action)) / d action with w ~ N(0, 1) -- the gradient
+    policy_loss.backward() sends into the policy (sac_cbf.py:147-158).  Also
+    unicycle (3 hazards) at the same size."""
+    from rcbf_sac import sac_cbf
+    rng = np.random.default_rng(seed)
+    out = {}
+
+    class A:
+        gp_model_size = 2000
+        cuda = False
+
+    class Agent:  # the two attributes RCBF_SAC.get_safe_action touches
+        pass
+
+    for name, Env in (("cars", SimulatedCarsEnv), ("uni3", UnicycleEnv)):
+        env = Env()
+        if name == "cars":
+            st, _ = _rollout_cars_states(SimulatedCarsEnv, B, rng)
+            obs = st.copy(); obs[:, ::2] /= 100.0; obs[:, 1::2] /= 30.0
+            n_u = 1
+        else:
+            env.hazards_locations = env.hazards_locations[:3]
+            x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+            rel = np.array([2.5, 2.5]) - x[:, :2]
+            c, s_ = np.cos(x[:, 2]), np.sin(x[:, 2])
+            comp = np.stack([rel[:, 0] * c + rel[:, 1] * s_, -rel[:, 0] * s_ + rel[:, 1] * c], 1)
+            comp /= np.linalg.norm(comp, axis=1, keepdims=True) + 0.001
+            obs = np.hstack([x[:, :2], c[:, None], s_[:, None], comp, np.exp(-np.linalg.norm(rel, axis=1))[:, None]])
+            n_u = 2
+        agent = Agent()
+        agent.cbf_layer = _patch_layer(diff_cbf_qp.CBFQPLayer(env, A(), gamma_b=gamma_b, k_d=1.5, l_p=0.03))
+        dm = dynamics.DynamicsModel(env, A())
+        obs32 = obs.astype(np.float32)
+        act = rng.uniform(-1, 1, (B, n_u)).astype(np.float32)
+        w = rng.standard_normal((B, n_u)).astype(np.float32)
+        a_t = torch.tensor(act, requires_grad=True)
+        safe = sac_cbf.RCBF_SAC.get_safe_action(agent, torch.tensor(obs32), a_t, dm)
+        (safe * torch.tensor(w)).sum().backward()
+        out.update({f"{name}_obs32": obs32, f"{name}_action": act, f"{name}_w": w,
+                    f"{name}_final": safe.detach().numpy(), f"{name}_grad_action": a_t.grad.numpy()})
+        if name == "uni3":
+            out["uni3_hazards"] = env.hazards_locations.astype(np.float64)
+    out["gamma_b"] = np.float64(gamma_b)
     return out
 
 
@@ -561,6 +649,8 @@ def main():
         "closed_loop_cars.npz": lambda: make_closed_loop(SimulatedCarsEnv, cbf_qp, dynamics),
         "dynamics.npz": lambda: make_dynamics(SimulatedCarsEnv, UnicycleEnv, dynamics),
         "model_rollouts.npz": lambda: make_model_rollouts(SimulatedCarsEnv, UnicycleEnv, dynamics),
+        "layer_f64_build.npz": lambda: make_f64_build(SimulatedCarsEnv, UnicycleEnv, diff_cbf_qp),
+        "sac_update_config5.npz": lambda: make_sac_update(SimulatedCarsEnv, UnicycleEnv, diff_cbf_qp, dynamics),
     }
     only = set(sys.argv[1:])
     for fname, fn in jobs.items():

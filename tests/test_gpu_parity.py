@@ -620,3 +620,38 @@ def test_pdipm_agrees_with_exact_solver_at_scale(mode):
     a = _layer(env, 20.0, 0).get_safe_action(*args)
     b = _layer(env, 20.0, 1).get_safe_action(*args)
     assert float((a - b).abs().max()) <= 1e-5
+
+
+@pytest.mark.parametrize("name,mode", [("cars", "SimulatedCars"), ("uni3", "Unicycle")])
+def test_sac_update_config5_golden(golden, name, mode):
+    """Config 5 (B = 4096, forward + backward) against the reference's own
+    RCBF_SAC.get_safe_action (sac_cbf.py:218-238) run on the same fp32
+    observations: safe action and d final / d action <= 1e-5."""
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.sac_cbf import get_safe_action
+    d = golden("sac_update_config5")
+    env = _env(mode, d.get(f"{name}_hazards"))
+    layer = _layer(env, float(d["gamma_b"]))
+    dyn = DynamicsModel(env, Args())
+    a = dev(d[f"{name}_action"]).requires_grad_(True)
+    out = get_safe_action(layer, dev(d[f"{name}_obs32"]), a, dyn)
+    (out * dev(d[f"{name}_w"])).sum().backward()
+    assert rel(out.detach().cpu().numpy(), d[f"{name}_final"]) <= 1e-5
+    assert rel(a.grad.cpu().numpy(), d[f"{name}_grad_action"]) <= 1e-5
+
+
+@pytest.mark.parametrize("name,mode", [("cars", "SimulatedCars"), ("uni3", "Unicycle"), ("uni5", "Unicycle")])
+def test_f64_build_variant_golden(golden, name, mode):
+    """The fp32-built HIP layer against the reference built in fp64
+    (torch.set_default_dtype(float64)), B = 4096: within 1e-4 (the build
+    precision alone moves the action by up to ~1e-4), and equal to
+    the fp32 oracle on the same inputs within 1e-5."""
+    d = golden("layer_f64_build")
+    g = lambda k: d[f"{name}_{k}"]  # noqa: E731
+    env = _env(mode, d.get(f"{name}_hazards"))
+    layer = _layer(env, float(d["gamma_b"]))
+    x, u, mu, sg = (g(k).astype(np.float32) for k in ("x", "u", "mu", "sigma"))
+    fin = layer.get_safe_action(dev(x), dev(u), dev(mu), dev(sg)).cpu().numpy()
+    assert rel(fin, g("final")) <= 1e-4
+    ref32, _ = O.safe_action_diff(mode, x, u, mu, sg, float(d["gamma_b"]), hazards=d.get(f"{name}_hazards"))
+    assert rel(fin, ref32) <= 1e-5

@@ -164,3 +164,39 @@ def test_model_rollout_step_vs_reference(golden):
         assert np.max(np.abs(r - d[nm + "_reward"])) <= 1e-13
         assert np.array_equal(mask, d[nm + "_mask"]) and np.array_equal(tn, d[nm + "_next_t"])
         assert (mask == 0).sum() >= 8  # the fixture exercises episode ends / goals
+
+
+@pytest.mark.parametrize("name,mode", [("cars", "SimulatedCars"), ("uni3", "Unicycle")])
+def test_sac_update_config5(golden, name, mode):
+    """Config 5 through the reference's own RCBF_SAC.get_safe_action
+    (sac_cbf.py:218-238) at B = 4096: the oracle's get_state(obs32) -> prior
+    -> safe action and its d final / d action equal the reference's."""
+    d = golden("sac_update_config5")
+    obs = d[f"{name}_obs32"]
+    hz = d.get(f"{name}_hazards")
+    s32 = O.get_state_f32(mode, obs)
+    mu, sg = O.predict_disturbance_prior(mode, obs.shape[0])
+    mu, sg = mu.astype(np.float32), sg.astype(np.float32)
+    fin, _ = O.safe_action_diff(mode, s32, d[f"{name}_action"], mu, sg, float(d["gamma_b"]), hazards=hz)
+    assert rel(fin, d[f"{name}_final"]) <= 1e-5
+    g, _ = O.safe_action_diff_grad(mode, s32, d[f"{name}_action"], mu, sg, float(d["gamma_b"]), d[f"{name}_w"],
+                                   hazards=hz)
+    assert rel(g, d[f"{name}_grad_action"]) <= 1e-5
+
+
+@pytest.mark.parametrize("name,mode", [("cars", "SimulatedCars"), ("uni3", "Unicycle"), ("uni5", "Unicycle")])
+def test_f64_build_variant(golden, name, mode):
+    """The reference built in fp64 (torch.set_default_dtype(float64)): the
+    exact QP on its fp64 normalised rows reproduces its z, and the shipped
+    fp32 build (what the oracle and the kernel compute) lands within 1e-4 of
+    its safe action -- the precision sensitivity SURVEY 7 measured."""
+    d = golden("layer_f64_build")
+    g = lambda k: d[f"{name}_{k}"]  # noqa: E731
+    Pd = np.diagonal(g("P"), axis1=1, axis2=2).astype(np.float64)
+    z, _, _, st = O.qp_exact(Pd, g("Gn"), g("hn"))
+    ok = st == 0
+    assert ok.mean() > 0.999 and rel(z[ok], g("z")[ok]) <= 1e-9
+    f32 = lambda k: g(k).astype(np.float32)  # noqa: E731
+    fin, _ = O.safe_action_diff(mode, f32("x"), f32("u"), f32("mu"), f32("sigma"), float(d["gamma_b"]),
+                                hazards=d.get(f"{name}_hazards"))
+    assert rel(fin, g("final")) <= 1e-4
