@@ -526,6 +526,45 @@ def generic_qp_rows(layer, dev):
                 "fwd_us": round(fms * 1e3, 2), "bwd_us": round(bms * 1e3, 2),
                 "fwd_GBs": round(B * (by_in + 4 * n) / fms / 1e6, 1),
                 "bwd_GBs": round(B * (2 * by_in + 4 * n) / bms / 1e6, 1)}
+    # the layer's own rows (diagonal P, q = 0, slack/actuator structure): solve_qp as
+    # get_safe_action calls it -- the closed-form path
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+
+    class LArgs:
+        cuda = True
+    B = 65536
+    for name, env in (("cars", BatchedSimulatedCarsEnv(4, device=dev)),
+                      ("unicycle3", BatchedUnicycleEnv(4, device=dev, hazards_locations=unicycle_hazards(3)))):
+        lay = CBFQPLayer(env, LArgs(), gamma_b=20.0)
+        if name == "cars":
+            x = torch.tensor([34., 30., 28., 30., 22., 30., 16., 35., 10., 30.], device=dev).repeat(B, 1)
+            x = x + torch.randn(B, 10, device=dev, generator=gen) * torch.tensor([3., 1.] * 5, device=dev)
+        else:
+            x = torch.cat([torch.rand(B, 2, device=dev, generator=gen) * 6 - 3,
+                           (torch.rand(B, 1, device=dev, generator=gen) * 2 - 1) * math.pi], 1)
+        u = torch.rand(B, env.n_u, device=dev, generator=gen) * 2 - 1
+        mu = torch.zeros(B, env.n_s, device=dev)
+        sg = torch.full((B, env.n_s), 0.2, device=dev)
+        P, q, G, h = (t.contiguous() for t in lay.get_cbf_qp_constraints(x, u, mu, sg))
+        n, m = G.shape[2], G.shape[1]
+        z = torch.empty(B, n, device=dev)
+        prm = ctypes.byref(lay._prm)
+
+        def fwd_l():
+            lib.rcbf_qp_solve(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(z),
+                              None, None, None, _lib.stream_of(dev))
+        gz = torch.randn(B, n, device=dev, generator=gen)
+        gP, gq, gG, gh = torch.empty_like(P), torch.empty_like(q), torch.empty_like(G), torch.empty_like(h)
+
+        def bwd_l():
+            lib.rcbf_qp_backward(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(gz),
+                                 _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh), _lib.stream_of(dev))
+        fms, bms = _time_graph(fwd_l, 20, dev), _time_graph(bwd_l, 20, dev)
+        by_in = 4 * (n * n + n + m * n + m)
+        out[f"qp_layer_rows_{name}_B{B}"] = {"fwd_us": round(fms * 1e3, 2), "bwd_us": round(bms * 1e3, 2),
+                                             "fwd_GBs": round(B * (by_in + 4 * n) / fms / 1e6, 1),
+                                             "bwd_GBs": round(B * (2 * by_in + 4 * n) / bms / 1e6, 1)}
     return out
 
 

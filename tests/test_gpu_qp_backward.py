@@ -131,3 +131,88 @@ def test_solve_qp_grad_composes_to_reference_grad(golden, fixture, mode):
         grad = ut.grad.cpu().numpy().astype(np.float64) + np.einsum(
             "bm,bmc->bc", ht.grad.cpu().numpy().astype(np.float64), _dh_du(mode, G.astype(np.float64)))
         assert rel(grad, d[tag + "_grad_u"]) <= 1e-5, tag
+
+
+@pytest.mark.parametrize("mode,k", [("SimulatedCars", 0), ("Unicycle", 1), ("Unicycle", 3), ("Unicycle", 5),
+                                    ("Unicycle", 8)])
+def test_structured_fast_path_equals_general_solver(mode, k):
+    """rcbf_qp_solve on the layer's own rows (diagonal P, q = 0, the slack /
+    actuator structure: CBFQPLayer.solve_qp as get_safe_action calls it,
+    diff_cbf_qp.py:74,81-109) takes the closed-form path when no multipliers
+    are requested; it equals the Goldfarb-Idnani path (taken when lam_out is
+    requested) and the oracle's exact optimum.  B = 65536 + a ragged tail,
+    rows normalised in-kernel; mixed waves (one lane breaking the structure)
+    fall back to the general solver."""
+    from rcbf_amd import _lib
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+    rng = np.random.default_rng(40 + k)
+    B = 65536 + 77
+    if mode == "SimulatedCars":
+        env = BatchedSimulatedCarsEnv(4)
+        from test_gpu_parity import _cars_states
+        x = _cars_states(4096, 3)[0][rng.integers(0, 4096, B)] + rng.normal(0, 0.3, (B, 10))
+        hz = None
+        mu, sg = np.zeros((B, 10)), np.tile(np.array(O.MAX_STD["SimulatedCars"]), (B, 1))
+    else:
+        hz = O.UNI["hazards"][:k] if k <= 5 else np.concatenate([O.UNI["hazards"], rng.uniform(-2.5, 2.5, (k - 5, 2))])
+        env = BatchedUnicycleEnv(4, hazards_locations=hz)
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        mu, sg = np.zeros((B, 3)), np.full((B, 3), 0.2)
+    layer = CBFQPLayer(env, Args(), gamma_b=20.0)
+    u = rng.uniform(-1, 1, (B, env.n_u))
+    P, q, G, h = layer.get_cbf_qp_constraints(dev(x), dev(u), dev(mu), dev(sg))
+    G[B - 3, 0, 0] = 0.25  # one lane of the ragged last wave breaks the structure
+    n, m = G.shape[2], G.shape[1]
+    s = _lib.stream_of(torch.device("cuda"))
+    lib = _lib.load()
+    z_fast = torch.empty(B, n, device="cuda")
+    z_gi = torch.empty(B, n, device="cuda")
+    lam = torch.empty(B, m, dtype=torch.float64, device="cuda")
+    st1 = torch.empty(B, dtype=torch.int32, device="cuda")
+    st2 = torch.empty(B, dtype=torch.int32, device="cuda")
+    assert lib.rcbf_qp_solve(ctypes.byref(layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1,
+                             _lib.ptr(z_fast), None, _lib.ptr(st1), None, s) == 0
+    assert lib.rcbf_qp_solve(ctypes.byref(layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1,
+                             _lib.ptr(z_gi), _lib.ptr(lam), _lib.ptr(st2), None, s) == 0
+    torch.cuda.synchronize()
+    ok = (st1 == 0) & (st2 == 0)
+    assert ok.float().mean().item() > 0.999
+    a, b = z_fast.double().cpu().numpy(), z_gi.double().cpu().numpy()
+    okn = ok.cpu().numpy()
+    assert rel(a[okn], b[okn]) <= 1e-5
+    Gn, hn, _ = O.normalize_rows(G.cpu().numpy(), h.cpu().numpy())
+    Pd = np.diagonal(P.cpu().numpy(), axis1=1, axis2=2).astype(np.float64)
+    sel = np.nonzero(okn)[0][::16]
+    zo, _, _, sto = O.qp_exact(Pd[sel], Gn[sel], hn[sel])
+    good = sto == 0
+    assert rel(a[sel][good], zo[good].astype(np.float32)) <= 1e-5
+
+
+@pytest.mark.parametrize("fixture,mode", [("cars_layer", "SimulatedCars"), ("unicycle3_layer", "Unicycle"),
+                                          ("unicycle5_layer", "Unicycle")])
+def test_structured_backward_vs_oracle(golden, fixture, mode):
+    """rcbf_qp_backward on the layer's own rows (the closed-form optimum and
+    multipliers from stationarity) equals the oracle's implicit-KKT
+    derivative for every gradient output on the non-degenerate rows, with and
+    without normalisation (4096 reference-built rows)."""
+    from rcbf_amd import _lib
+    d = golden(fixture)
+    G, h, P, q = (d["rand" + k].astype(np.float32) for k in ("_G", "_h", "_P", "_q"))
+    B, m, n = G.shape
+    rng = np.random.default_rng(3)
+    w = rng.normal(0, 1, (B, n)).astype(np.float32)
+    layer = _layer()
+    lib = _lib.load()
+    for normalize in (0, 1):
+        want = O.qp_backward(P.astype(np.float64), q.astype(np.float64), G, h, bool(normalize), w)
+        Pd, qd, Gd, hd, wd = dev(P), dev(q), dev(G), dev(h), dev(w)
+        gP, gq, gG, gh = torch.empty_like(Pd), torch.empty_like(qd), torch.empty_like(Gd), torch.empty_like(hd)
+        assert lib.rcbf_qp_backward(ctypes.byref(layer._prm), B, n, m, _lib.ptr(Pd), _lib.ptr(qd), _lib.ptr(Gd),
+                                    _lib.ptr(hd), normalize, _lib.ptr(wd), _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG),
+                                    _lib.ptr(gh), _lib.stream_of(Gd.device)) == 0
+        torch.cuda.synchronize()
+        ok = _non_degenerate(P.astype(np.float64), q.astype(np.float64), G, h, normalize)
+        assert ok.mean() > 0.9
+        for k, got in (("P", gP), ("q", gq), ("G", gG), ("h", gh)):
+            assert rel(got.cpu().numpy()[ok], want[k][ok]) <= 1e-5, (k, normalize)
