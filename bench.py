@@ -474,16 +474,30 @@ def sac_update_safe_action(env, layer, dev):
             (out * w).sum().backward()
             return uu.grad
 
-        for _ in range(5):
-            eager()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        n = 50
-        for _ in range(n):
-            eager()
-        torch.cuda.synchronize()
-        a_us = (time.perf_counter() - t0) * 1e6 / n
-        res[f"sac_safe_action_fwd_bwd_B{B}"] = {"kernel_us": round(k_us, 2), "autograd_us": round(a_us, 1)}
+        def torch_floor():  # the same loss around a torch-only stand-in op: torch's own autograd cost
+            uu = u.clone().requires_grad_(True)
+            (torch.clamp(uu + 0.1, -10.0, 10.0) * w).sum().backward()
+            return uu.grad
+
+        def per_call(fn, n=50):
+            for _ in range(5):
+                fn()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                fn()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) * 1e6 / n
+
+        a_us = per_call(eager)
+        op, _lib._torch_op = _lib._torch_op, None  # the Python autograd.Function path, for comparison
+        try:
+            p_us = per_call(eager)
+        finally:
+            _lib._torch_op = op
+        res[f"sac_safe_action_fwd_bwd_B{B}"] = {"kernel_us": round(k_us, 2), "autograd_us": round(a_us, 1),
+                                                "python_function_us": round(p_us, 1),
+                                                "torch_only_floor_us": round(per_call(torch_floor), 1)}
     return res
 
 

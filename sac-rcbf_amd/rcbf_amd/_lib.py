@@ -123,6 +123,7 @@ def load():
     if lib.rcbf_abi_version() != ABI_VERSION or lib.rcbf_params_size() != ctypes.sizeof(RcbfParams):
         raise RuntimeError("librcbf_hip.so ABI mismatch (rebuild with `python __graft_entry__.py build`)")
     _bind_fast(lib)
+    _bind_torch_op(lib)
     _lib = lib
     return lib
 
@@ -143,6 +144,30 @@ def _bind_fast(lib):
         return
     _rcbf_fast.bind(*(entry_address(lib, n) for n in FAST_ENTRY_POINTS))
     _fast = _rcbf_fast
+
+
+TORCH_OP_ENTRY_POINTS = ("rcbf_safe_action", "rcbf_safe_action_backward", "rcbf_obs_safe_action",
+                         "rcbf_obs_safe_action_backward")
+_torch_op = None
+
+
+def _bind_torch_op(lib):
+    """The C++ autograd op of the safe action (csrc/rcbf_torch_op.cpp,
+    optional), bound like the CPython binding to THIS library copy."""
+    global _torch_op
+    try:
+        from . import _rcbf_torch
+    except ImportError:
+        _torch_op = None
+        return
+    _rcbf_torch.bind(*(entry_address(lib, n) for n in TORCH_OP_ENTRY_POINTS))
+    _torch_op = _rcbf_torch
+
+
+def torch_op():
+    """The C++ autograd op bound to the loaded library, or None if not built."""
+    load()
+    return _torch_op
 
 
 def entry_address(lib, name):

@@ -90,6 +90,19 @@ class _SafeAction(torch.autograd.Function):
         return None, None, gu, None, None, None
 
 
+def safe_action_op(layer, x, u, mu, sigma, from_obs=False):
+    """final = clamp(u + QP(u)[:n_u]) with autograd w.r.t. u: the C++ autograd
+    op (csrc/rcbf_torch_op.cpp) when it is built, else the Python Function;
+    both launch the same two C-ABI entry points and raise the reference's
+    Exception('QP Failed to solve') after one flag read."""
+    op = _lib.torch_op()
+    if op is None:
+        return _SafeAction.apply(layer, x, u, mu, sigma, from_obs)
+    flag = _fail_flag(layer, x.device) if layer.check_failures else None
+    return op.safe_action(x, u, mu, sigma, ctypes.addressof(layer._prm), 0 if flag is None else flag.data_ptr(),
+                          bool(from_obs))
+
+
 class _QP(torch.autograd.Function):
     """z = QP(P, q, G, h) (optionally on row-normalised [G h]); backward is
     rcbf_qp_backward: the implicit-KKT adjoint on the exact active set (what
@@ -172,7 +185,7 @@ class CBFQPLayer:
         else:
             u = _f32(action_batch, dev)
         self._check_shapes(x, u, mu, sig)
-        final_action = _SafeAction.apply(self, x, u, mu, sig)
+        final_action = safe_action_op(self, x, u, mu, sig)
         if final_action.device != out_device:
             final_action = final_action.to(out_device)
         return final_action if not expand_dims else final_action.squeeze(0)

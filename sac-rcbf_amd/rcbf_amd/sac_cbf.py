@@ -12,7 +12,7 @@ the device and feed CBFQPLayer.get_safe_action.
 """
 import torch
 
-from .diff_cbf_qp import CBFQPLayer, _SafeAction, _dev, _f32
+from .diff_cbf_qp import CBFQPLayer, _dev, _f32, safe_action_op
 
 
 def get_safe_action(cbf_layer, obs_batch, action_batch, dynamics_model):
@@ -41,7 +41,7 @@ def get_safe_action(cbf_layer, obs_batch, action_batch, dynamics_model):
     if obs.dim() != 2 or obs.shape[1] != n_o or u.shape != (obs.shape[0], cbf_layer.action_dim):
         raise ValueError(f"expected obs (B,{n_o}) and action (B,{cbf_layer.action_dim}), got "
                          f"{tuple(obs.shape)} / {tuple(u.shape)}")
-    out = _SafeAction.apply(cbf_layer, obs, u, None, None, True)
+    out = safe_action_op(cbf_layer, obs, u, None, None, True)
     if out.device != out_device:
         out = out.to(out_device)
     return out.squeeze(0) if expand else out

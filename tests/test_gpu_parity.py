@@ -655,3 +655,53 @@ def test_f64_build_variant_golden(golden, name, mode):
     assert rel(fin, g("final")) <= 1e-4
     ref32, _ = O.safe_action_diff(mode, x, u, mu, sg, float(d["gamma_b"]), hazards=d.get(f"{name}_hazards"))
     assert rel(fin, ref32) <= 1e-5
+
+
+@pytest.mark.parametrize("mode", ["SimulatedCars", "Unicycle"])
+def test_torch_op_matches_python_function(mode, monkeypatch):
+    """The C++ autograd op (csrc/rcbf_torch_op.cpp) and the Python
+    autograd.Function launch the same kernels: bit-identical safe actions and
+    d/d action, through RCBF_SAC.get_safe_action (obs input) and
+    CBFQPLayer.get_safe_action (state input); both raise the reference's
+    Exception('QP Failed to solve') on a NaN state and recover after it."""
+    from rcbf_amd import _lib
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.sac_cbf import get_safe_action
+    assert _lib.torch_op() is not None, "_rcbf_torch not built (run __graft_entry__.build())"
+    rng = np.random.default_rng(9)
+    B = 512
+    hz = O.UNI["hazards"][:3] if mode == "Unicycle" else None
+    env = _env(mode, hz)
+    layer = _layer(env, 20.0)
+    dyn = DynamicsModel(env, Args())
+    if mode == "SimulatedCars":
+        x, _, _ = _cars_states(B, 4)
+        obs = O.cars_obs(x).astype(np.float32)
+    else:
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        obs = O.uni_obs(x).astype(np.float32)
+    s32 = O.get_state_f32(mode, obs)
+    mu, sg = (v.astype(np.float32) for v in O.predict_disturbance_prior(mode, B))
+    u = rng.uniform(-1, 1, (B, env.n_u)).astype(np.float32)
+    w = dev(rng.normal(0, 1, (B, env.n_u)))
+
+    def run():
+        a = dev(u).requires_grad_(True)
+        o1 = get_safe_action(layer, dev(obs), a, dyn)
+        (o1 * w).sum().backward()
+        b = dev(u).requires_grad_(True)
+        o2 = layer.get_safe_action(dev(s32), b, dev(mu), dev(sg))
+        (o2 * w).sum().backward()
+        return [o1.detach(), a.grad, o2.detach(), b.grad]
+
+    cpp = run()
+    monkeypatch.setattr(_lib, "_torch_op", None)
+    py = run()
+    monkeypatch.undo()
+    for p, q in zip(cpp, py):
+        assert torch.equal(p, q)
+    bad = s32.copy()
+    bad[3, 2] = np.nan
+    with pytest.raises(Exception, match="QP Failed to solve"):
+        layer.get_safe_action(dev(bad), dev(u), dev(mu), dev(sg))
+    assert torch.equal(layer.get_safe_action(dev(s32), dev(u), dev(mu), dev(sg)), cpp[2])
