@@ -10,172 +10,82 @@
 
 namespace rcbf {
 
-#ifndef RCBF_BLOCK
-#define RCBF_BLOCK 256
-#endif
-constexpr int kBlock = RCBF_BLOCK;
-// Ablation switches for performance studies only (scripts/build_variants.sh
-// builds them into separate libraries; the product build uses 0):
-//   1 = no QP (u_qp = 0), 2 = no rows/normalise/QP, 4 = no env dynamics,
-//   8 = no observation maths, 16 = no auto-reset
-#ifndef RCBF_ABLATE
-#define RCBF_ABLATE 0
-#endif
-constexpr int kAblate = RCBF_ABLATE;
-
-// Envs per 64-lane wavefront in the env kernels (performance study knob:
-// 32 leaves the upper half of every wave idle and doubles the wave count).
-#ifndef RCBF_ENVS_PER_WAVE
-#define RCBF_ENVS_PER_WAVE 64
-#endif
-constexpr int kEnvsPerWave = RCBF_ENVS_PER_WAVE;
-constexpr int kEnvsPerBlock = kBlock / 64 * kEnvsPerWave;
+constexpr int kBlock = 256;
 
 inline unsigned grid_for(int64_t B) { return (unsigned)((B + kBlock - 1) / kBlock); }
-inline unsigned grid_for_envs(int64_t B) { return (unsigned)((B + kEnvsPerBlock - 1) / kEnvsPerBlock); }
+inline unsigned grid_for_envs(int64_t B) { return grid_for(B); }
 
-// env index of this lane in the env kernels; -1 for an idle lane
-__device__ __forceinline__ int64_t env_index() {
-    if constexpr (kEnvsPerWave == 64) {
-        return (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    } else {
-        int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        if (lane >= kEnvsPerWave) return -1;
-        return (int64_t)blockIdx.x * kEnvsPerBlock + wave * kEnvsPerWave + lane;
-    }
-}
+// env index of this lane in the env kernels: one env per lane
+__device__ __forceinline__ int64_t env_index() { return (int64_t)blockIdx.x * kBlock + threadIdx.x; }
 
-// Output store flavour of the env kernels (performance study knob):
-//   0 = plain stores (lines stay dirty in the XCD's L2 until the kernel-end
-//       write-back), 1 = write-through `sc1` stores (agent-scope relaxed
-//       atomic stores: the line leaves L2 as it is written), 2 = `nt` stores
-//       (default: with whole-line stores it is the fastest, profiles/r01),
-//       3 = the 16-byte stores (state pairs, staged observation chunks)
-//       write-through `sc1`, so their lines are not left dirty for the
-//       kernel-end L2 write-back; the narrow ones `nt`.
-#ifndef RCBF_STORE_MODE
-#define RCBF_STORE_MODE 2
-#endif
-constexpr int kStoreMode = RCBF_STORE_MODE;
-// with RCBF_STORE_MODE=2: also store the staged observation chunks `nt`
-#ifndef RCBF_OBS_NT
-#define RCBF_OBS_NT 1
-#endif
-constexpr bool kObsNt = RCBF_OBS_NT;
-
-// 1 = store the safe action right after the QP so its write overlaps the env
-// step (otherwise all outputs are stored after the observation).
-#ifndef RCBF_EARLY_STORE
-#define RCBF_EARLY_STORE 0
-#endif
-
-// one 16-byte write-through store: global_store_dwordx4 ... sc1 (the s_nop
-// covers the store-data hazard the compiler cannot see inside the asm)
-__device__ __forceinline__ void st_wt16(void* p, uint4 v) {
-    typedef unsigned u4 __attribute__((ext_vector_type(4)));
-    const u4 w = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
-}
-
+// Memory policy of the env kernels: every once-read input is an `nt` load and
+// every output an `nt` store (with the whole-line stores below the fastest of
+// the flavours measured: plain, write-through sc1, nt; profiles/r01).
 template <typename T>
 __device__ __forceinline__ void st_out(T* p, T v) {
-    if constexpr (kStoreMode == 1) {
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if constexpr (kStoreMode == 2 || kStoreMode == 3) {
-        __builtin_nontemporal_store(v, p);
-    } else {
-        *p = v;
-    }
+    __builtin_nontemporal_store(v, p);
 }
 
-// 16-byte store (staged obs chunks), same flavours except sc1 -> plain
+// 16-byte store (staged observation chunks)
 __device__ __forceinline__ void st_out4(float* p, float4 v) {
     typedef float f4 __attribute__((ext_vector_type(4)));
-    if constexpr (kStoreMode == 3) {
-        st_wt16(p, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)));
-    } else if constexpr (kStoreMode == 2 && kObsNt) {
-        f4 w = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(w, reinterpret_cast<f4*>(p));
-    } else {
-        *reinterpret_cast<float4*>(p) = v;
-    }
+    f4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<f4*>(p));
 }
 
 // 16-byte f64 pair store (env state pairs)
 __device__ __forceinline__ void st_out2d(double* p, double a, double b) {
     typedef double d2 __attribute__((ext_vector_type(2)));
-    if constexpr (kStoreMode == 1) {
-        st_out(p, a);
-        st_out(p + 1, b);
-    } else if constexpr (kStoreMode == 3) {
-        const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
-        st_wt16(p, make_uint4((uint32_t)ua, (uint32_t)(ua >> 32), (uint32_t)ub, (uint32_t)(ub >> 32)));
-    } else if constexpr (kStoreMode == 2) {
-        d2 w = {a, b};
-        __builtin_nontemporal_store(w, reinterpret_cast<d2*>(p));
-    } else {
-        *reinterpret_cast<double2*>(p) = make_double2(a, b);
-    }
+    d2 w = {a, b};
+    __builtin_nontemporal_store(w, reinterpret_cast<d2*>(p));
 }
 
-// Input load flavour: 0 = plain, 2 = `nt` (once-read streams)
-#ifndef RCBF_LOAD_MODE
-#define RCBF_LOAD_MODE 2
-#endif
 template <typename T>
 __device__ __forceinline__ T ld_in(const T* p) {
-    if constexpr (RCBF_LOAD_MODE == 2)
-        return __builtin_nontemporal_load(p);
-    else
-        return *p;
+    return __builtin_nontemporal_load(p);
 }
+
 __device__ __forceinline__ double2 ld_in2(const double* p) {
     typedef double d2 __attribute__((ext_vector_type(2)));
-    d2 v;
-    if constexpr (RCBF_LOAD_MODE == 2)
-        v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(p));
-    else
-        v = *reinterpret_cast<const d2*>(p);
+    d2 v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(p));
     return make_double2(v.x, v.y);
 }
 
-// 8-byte pair store (obs rows): one dwordx2 store in every flavour
+// 8-byte pair store (obs rows): one dwordx2 store
 __device__ __forceinline__ void st_out2(float* p, float a, float b) {
-    if constexpr (kStoreMode == 0) {
-        *reinterpret_cast<float2*>(p) = make_float2(a, b);
-    } else {
-        union {
-            float f[2];
-            uint64_t u;
-        } w;
-        w.f[0] = a;
-        w.f[1] = b;
-        st_out<uint64_t>(reinterpret_cast<uint64_t*>(p), w.u);
-    }
+    union {
+        float f[2];
+        uint64_t u;
+    } w;
+    w.f[0] = a;
+    w.f[1] = b;
+    st_out<uint64_t>(reinterpret_cast<uint64_t*>(p), w.u);
 }
 
-// Diagnostic build only (-DRCBF_STAMPS=1): lane 0 of every wave records
-// s_memtime at phase boundaries of the fused step into the status_out buffer
-// reinterpreted as uint64 [wave][16].  Never part of the product build.
-#ifndef RCBF_STAMPS
-#define RCBF_STAMPS 0
-#endif
-#if RCBF_STAMPS
-#define RCBF_STAMP(buf, j, drain)                                                          \
-    do {                                                                                   \
-        if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                       \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-        unsigned long long t_;                                                             \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-        if ((threadIdx.x & 63) == 0 && (buf))                                              \
-            (buf)[((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + (j)] = t_; \
-    } while (0)
-#else
-#define RCBF_STAMP(buf, j, drain) \
-    do {                          \
-    } while (0)
-#endif
+// Phase timestamps of the fused step for the study build only
+// (csrc/study/rcbf_stamps.hip, scripts/stamps.py): lane 0 of every wave
+// records s_memtime at phase boundaries into buf as uint64 [wave][16].  The
+// product kernels use Stamps<false>, whose mark() compiles to nothing.
+template <bool ON>
+struct Stamps {
+    unsigned long long* buf = nullptr;
+    __device__ __forceinline__ void mark(int j, bool drain) const {
+        if constexpr (ON) {
+            if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            unsigned long long t;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if ((threadIdx.x & 63) == 0 && buf) buf[((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + j] = t;
+        }
+    }
+    __device__ __forceinline__ void count(int j, bool lane_flag) const {
+        if constexpr (ON) {
+            unsigned long long b = __ballot(lane_flag);
+            if ((threadIdx.x & 63) == 0 && buf) buf[((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + j] = __popcll(b);
+        }
+    }
+};
 
 // ---------------------------------------------------------------------------
 // mode traits
@@ -257,18 +167,12 @@ struct LayerState {
 // build -> normalise -> fp64 QP -> .float() -> clamp.
 // NEED_LAM: the caller needs the multipliers and the active set (backward);
 // otherwise the cars path uses the 1-D exact solver (cars_qp_1d).
-template <int SOLVER, int MODE, int K, bool NEED_LAM = false>
+template <int SOLVER, int MODE, int K, bool NEED_LAM = false, bool ST = false>
 __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const float* xs, const float* u,
                                               const float* mu, const float* sig, float* u_final,
-                                              LayerState<MODE, K>& L, unsigned long long* stamps = nullptr,
+                                              LayerState<MODE, K>& L, const Stamps<ST>& stamps = {},
                                               const float* cs_row = nullptr) {
     using D = Dims<MODE, K>;
-    if constexpr ((kAblate & 2) != 0) {
-#pragma unroll
-        for (int c = 0; c < D::NU; ++c) u_final[c] = u[c] + xs[c] * 1e-30f;
-        L.qp.status = RCBF_QP_OK;
-        return;
-    }
     diff_rows<MODE, K>(prm, xs, u, mu, sig, L.G, L.h, cs_row);
 #pragma unroll
     for (int r = 0; r < D::M; ++r) {
@@ -277,25 +181,21 @@ __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const floa
         for (int k = 0; k < D::N; ++k) L.Graw[r][k] = L.G[r][k];
     }
     normalize_rows<D::N, D::M, float>(L.G, L.h, L.Nrm, L.ish);
-    RCBF_STAMP(stamps, 3, false);
+    stamps.mark(3, false);
     PMat<D::N, true> pm;
     double pd[D::N], q[D::N];
     diff_P<MODE>(pd);
 #pragma unroll
     for (int k = 0; k < D::N; ++k) q[k] = 0.0;
     pmat_set_diag<D::N>(pm, pd);
-    if constexpr ((kAblate & 1) != 0) {
-#pragma unroll
-        for (int k = 0; k < D::N; ++k) L.qp.z[k] = 1e-30 * (double)(L.G[0][k] + L.h[k % D::M]);
-        L.qp.status = RCBF_QP_OK;
-    } else if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && SOLVER == RCBF_SOLVER_ACTIVE_SET && !NEED_LAM) {
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && SOLVER == RCBF_SOLVER_ACTIVE_SET && !NEED_LAM) {
         cars_qp_1d<float>(pm, L.G, L.h, L.qp.z, L.qp.status);
     } else if constexpr (MODE == RCBF_MODE_UNICYCLE && SOLVER == RCBF_SOLVER_ACTIVE_SET && !NEED_LAM) {
         uni_qp_2d<K, float>(pm, L.G, L.h, L.qp.z, L.qp.status);
     } else {
         qp_solve<SOLVER, D::N, D::M, true, float>(pm, q, L.G, L.h, prm.max_iter, prm.eps, L.qp);
     }
-    RCBF_STAMP(stamps, 4, false);
+    stamps.mark(4, false);
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) {
         float v = u[c] + (float)L.qp.z[c];
@@ -333,10 +233,7 @@ __device__ __forceinline__ void env_reset_one(const double* noise, int64_t i, ui
 
 template <int MODE>
 __device__ __forceinline__ void env_obs(const double* xs, double* o) {
-    if constexpr ((kAblate & 8) != 0) {
-#pragma unroll
-        for (int k = 0; k < Dims<MODE, 1>::NO; ++k) o[k] = xs[k % Dims<MODE, 1>::NS];
-    } else if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
         cars_obs(xs, o);
     } else {
         uni_obs(xs, o);
@@ -377,13 +274,13 @@ __device__ __forceinline__ void state_from_env(const double* xs, float* s32) {
 // The episode counter is only touched when the env resets.
 // obs_cache (unicycle): cos/sin/goal distance of the post-step state, valid
 // unless the env was reset (then obs_cache[3] = 0 and the obs is recomputed).
-template <int SOLVER, int MODE, int K>
+template <int SOLVER, int MODE, int K, bool ST = false>
 __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i, double* xs, double& a, int& st,
                                               uint32_t* episode, const float* us, const float* m, const float* s,
                                               float* uf, float& rew, float& cst, bool& dn, bool& gm, int& status,
                                               int auto_reset, uint64_t seed, int64_t off,
-                                              unsigned long long* stamps = nullptr, double* obs_cache = nullptr,
-                                              float* u_out = nullptr, bool ep_pre = false, uint32_t ep0 = 0) {
+                                              const Stamps<ST>& stamps = {}, double* obs_cache = nullptr,
+                                              bool ep_pre = false, uint32_t ep0 = 0) {
     using D = Dims<MODE, K>;
     float s32[D::NS];
     float cs_row[2];
@@ -394,32 +291,13 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
     } else {
         state_from_env<MODE>(xs, s32);
     }
-    RCBF_STAMP(stamps, 2, false);
+    stamps.mark(2, false);
     LayerState<MODE, K> L;
-    layer_forward<SOLVER, MODE, K>(prm, s32, us, m, s, uf, L, stamps,
-                                   MODE == RCBF_MODE_UNICYCLE ? cs_row : nullptr);
+    layer_forward<SOLVER, MODE, K, false, ST>(prm, s32, us, m, s, uf, L, stamps,
+                                              MODE == RCBF_MODE_UNICYCLE ? cs_row : nullptr);
     status = L.qp.status;
-    // issue the safe-action store now so its write overlaps the env step
-    if (u_out) {
-#pragma unroll
-        for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
-    }
-#if RCBF_STAMPS
-    {
-        unsigned long long fb = __ballot(L.qp.iters == 1);
-        if ((threadIdx.x & 63) == 0 && stamps)
-            stamps[((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + 9] = __popcll(fb);
-    }
-#endif
-    if constexpr ((kAblate & 4) != 0) {
-#pragma unroll
-        for (int k = 0; k < D::NS; ++k) xs[k] += 1e-3 * (double)uf[0];
-        st += 1;
-        rew = uf[0];
-        cst = 0.0f;
-        dn = st >= 300;
-        gm = false;
-    } else if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+    stamps.count(9, uf[0] != us[0]);  // lanes whose action the filter changed
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
         CarsStepOut o;
         cars_env_step<float>(prm, xs, a, st, uf[0], o);
         rew = o.reward;
@@ -440,8 +318,8 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
             obs_cache[3] = 1.0;
         }
     }
-    RCBF_STAMP(stamps, 5, false);
-    if (auto_reset && dn && (kAblate & 16) == 0) {
+    stamps.mark(5, false);
+    if (auto_reset && dn) {
         // ep_pre: the caller loaded episode[i] with the state (reset_foreseeable)
         uint32_t ep = episode ? (ep_pre ? ep0 : episode[i]) + 1u : 0u;
         if (episode) episode[i] = ep;

@@ -1317,11 +1317,7 @@ __device__ __forceinline__ void qp_solve(const PMat<N, DIAG>& pm, const double* 
             out.iters = its;
         }
     } else if constexpr (SOLVER == RCBF_SOLVER_ACTIVE_SET && N == 2 && DIAG) {
-#if defined(RCBF_ENUM2_FP64_ONLY)
-        enum2_solve<M, R>(pm, G, h, out);
-#else
         enum2_solve_fast<M, R>(pm, G, h, out);
-#endif
     } else {
         gi_solve<N, M, DIAG, R>(pm, q, G, h, max_iter > 0 ? max_iter : 4 * (M + N) + 8, out);
     }
@@ -1807,31 +1803,19 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
     }
 }
 
-// Reset draw precision.  1 (default): Box-Muller on 24-bit uniforms with the
-// hardware fp32 log2/cos -- ~10 instructions instead of ~170 for the fp64
-// libm path; the reset branch is on the critical path of whichever wave
-// holds a resetting env, and this took the cars step at SURVEY start states
-// from 5.3 to 4.9 us (profiles/r01).  Statistically a N(0,1) draw either way
-// (|z| <= 5.8 with 24-bit uniforms).
-#ifndef RCBF_NORMAL_F32
-#define RCBF_NORMAL_F32 1
-#endif
+// Reset draw: Box-Muller on 24-bit uniforms with the hardware fp32
+// log2/cos -- ~10 instructions instead of ~170 for an fp64 libm path; the
+// reset branch is on the critical path of whichever wave holds a resetting
+// env, and this took the cars step at SURVEY start states from 5.3 to 4.9 us
+// (profiles/r01).  Statistically a N(0,1) draw (|z| <= 5.8 with 24-bit
+// uniforms); restated by oracle.normal_draw.
 __device__ __forceinline__ double normal_draw(uint64_t seed, uint64_t env, uint32_t episode) {
     uint32_t c[4] = {(uint32_t)env, (uint32_t)(env >> 32), episode, 0x5AFEu};
     philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    // two 53-bit uniforms in (0,1] -> Box-Muller
-    uint64_t a = ((uint64_t)c[0] << 21) ^ (uint64_t)c[1];
-    uint64_t b = ((uint64_t)c[2] << 21) ^ (uint64_t)c[3];
-#if RCBF_NORMAL_F32
     // hardware fp32 transcendentals (v_log_f32, v_cos_f32 takes revolutions)
     float f1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);
     float f2 = (float)(c[2] >> 8) * (1.0f / 16777216.0f);
     return (double)(__builtin_sqrtf(-2.0f * __builtin_amdgcn_logf(f1) * 0.69314718f) * __builtin_amdgcn_cosf(f2));
-#else
-    double u1 = ((double)(a & ((1ull << 53) - 1)) + 1.0) * (1.0 / 9007199254740992.0);
-    double u2 = (double)(b & ((1ull << 53) - 1)) * (1.0 / 9007199254740992.0);
-    return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);  // cospi: no 2*pi range reduction
-#endif
 }
 
 __device__ __forceinline__ void cars_reset_state(double* xs, double noise) {

@@ -1,0 +1,163 @@
+// rcbf_safe_step.hpp -- the fused safe step kernel (the hot path bench.py
+// measures) and the env-state / observation memory helpers it shares with
+// the env kernels.  Included by rcbf_env.hip (the product instantiation) and
+// by csrc/study/rcbf_stamps.hip (the phase-timing study build).
+//
+// Env state is component-PAIR-major in HBM (see rcbf_common.hpp): one env per
+// lane, each lane moves 16 B per component pair, and a wavefront's load or
+// store of one pair is one contiguous 1 KiB access (dwordx4).  The fused step
+// reads x, t, step, u_RL and writes x', t', step', obs (AoS, the policy's
+// (B, n_o) input), u, reward, cost, done; the episode counter is touched only
+// on resets.
+#pragma once
+
+#include "rcbf_common.hpp"
+
+namespace rcbf {
+
+template <int MODE>
+__device__ __forceinline__ void load_state(const double* x, int64_t B, int64_t i, double* xs) {
+    constexpr int NS = Dims<MODE, 1>::NS;
+#pragma unroll
+    for (int p = 0; p < NS / 2; ++p) {
+        double2 v = ld_in2(&x[2 * (p * B + i)]);
+        xs[2 * p] = v.x;
+        xs[2 * p + 1] = v.y;
+    }
+    if constexpr (NS % 2) xs[NS - 1] = ld_in(&x[(NS - 1) * B + i]);
+}
+
+template <int MODE>
+__device__ __forceinline__ void store_state(double* x, int64_t B, int64_t i, const double* xs) {
+    constexpr int NS = Dims<MODE, 1>::NS;
+#pragma unroll
+    for (int p = 0; p < NS / 2; ++p) st_out2d(&x[2 * (p * B + i)], xs[2 * p], xs[2 * p + 1]);
+    if constexpr (NS % 2) st_out(&x[(NS - 1) * B + i], xs[NS - 1]);
+}
+
+template <int MODE>
+__device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double* xs,
+                                            const double* obs_cache = nullptr) {
+    constexpr int NO = Dims<MODE, 1>::NO;
+    double o[NO];
+    if constexpr (MODE == RCBF_MODE_UNICYCLE) {
+        if (obs_cache && obs_cache[3] != 0.0)
+            uni_obs_cs(xs, obs_cache[0], obs_cache[1], obs_cache[2], o);
+        else
+            env_obs<MODE>(xs, o);
+    } else {
+        env_obs<MODE>(xs, o);
+    }
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+        float* ov = obs + i * NO;  // 40 B rows, 8 B aligned
+#pragma unroll
+        for (int k = 0; k < NO / 2; ++k) st_out2(ov + 2 * k, (float)o[2 * k], (float)o[2 * k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NO; ++k) st_out(&obs[i * NO + k], (float)o[k]);
+    }
+}
+
+// Observation store through LDS: a full wave's 64 obs rows are one
+// contiguous (64*NO*4)-byte block; lanes write their rows into LDS, then
+// store the block as 16-byte chunks, chunk c by lane c%64 -- every store
+// instruction covers whole contiguous lines (cars: 3 dwordx4 instead of 5
+// strided dwordx2).  Partial or unaligned waves take the per-lane path.
+template <int MODE>
+__device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_t B, const double* xs,
+                                                   const double* obs_cache, float* lds_wave) {
+    constexpr int NO = Dims<MODE, 1>::NO;
+    const int lane = threadIdx.x & 63;
+    const int64_t base = i - lane;
+    const bool full = (base + 64 <= B) && ((reinterpret_cast<uintptr_t>(obs) & 15) == 0);
+    if (!full) {
+        store_obs32<MODE>(obs, i, xs, obs_cache);
+        return;
+    }
+    double o[NO];
+    if constexpr (MODE == RCBF_MODE_UNICYCLE) {
+        if (obs_cache && obs_cache[3] != 0.0)
+            uni_obs_cs(xs, obs_cache[0], obs_cache[1], obs_cache[2], o);
+        else
+            env_obs<MODE>(xs, o);
+    } else {
+        env_obs<MODE>(xs, o);
+    }
+    if constexpr (NO % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < NO / 2; ++k)
+            *reinterpret_cast<float2*>(&lds_wave[lane * NO + 2 * k]) = make_float2((float)o[2 * k], (float)o[2 * k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NO; ++k) lds_wave[lane * NO + k] = (float)o[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    constexpr int CH = NO * 16;  // 16-byte chunks in the wave's block
+    const float4* src = reinterpret_cast<const float4*>(lds_wave);
+    float* dst = obs + base * NO;
+#pragma unroll
+    for (int j = 0; j < (CH + 63) / 64; ++j) {
+        const int c = j * 64 + lane;
+        if (CH % 64 == 0 || c < CH) st_out4(dst + 4 * c, src[c]);
+    }
+}
+
+// The fused safe step (rcbf_safe_step): one env per lane.  ST = true only in
+// the study build (csrc/study/rcbf_stamps.hip), which records phase
+// timestamps into `stamps`; the product instantiation ignores it.
+template <int SOLVER, int MODE, int K, bool ST = false>
+__global__ void __launch_bounds__(kBlock) k_safe_step(rcbf_params prm, int64_t B, double* __restrict__ x,
+                                                      double* __restrict__ aux, int32_t* __restrict__ step,
+                                                      uint32_t* __restrict__ episode, const float* __restrict__ u_rl,
+                                                      const float* __restrict__ mu, const float* __restrict__ sigma,
+                                                      float* __restrict__ obs_out, float* __restrict__ u_out,
+                                                      float* __restrict__ reward, float* __restrict__ cost,
+                                                      uint8_t* __restrict__ done, uint8_t* __restrict__ goal_met,
+                                                      int32_t* __restrict__ status_out, int32_t* fail_flag,
+                                                      int auto_reset, uint64_t seed, int64_t off,
+                                                      unsigned long long* stamp_buf = nullptr) {
+    using D = Dims<MODE, K>;
+    int64_t i = env_index();
+    if (i >= B) return;
+    Stamps<ST> stamps;
+    stamps.buf = stamp_buf;
+    stamps.mark(0, false);
+    double xs[D::NS];
+    load_state<MODE>(x, B, i, xs);
+    double a = ld_in(&aux[i]);
+    int st = ld_in(&step[i]);
+    float us[D::NU], m[D::NS], s[D::NS], uf[D::NU];
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) us[c] = ld_in(&u_rl[i * D::NU + c]);
+    const bool ep_pre = episode && reset_foreseeable<MODE>(st, a);
+    uint32_t ep0 = 0;
+    if (ep_pre) ep0 = episode[i];
+#pragma unroll
+    for (int k = 0; k < D::NS; ++k) {
+        m[k] = mu ? mu[i * D::NS + k] : 0.0f;
+        s[k] = sigma ? sigma[i * D::NS + k] : prior_sigma<MODE>(k);
+    }
+    float rew, cst;
+    bool dn, gm;
+    int status;
+    stamps.mark(1, true);
+    double oc[4] = {0.0, 0.0, 0.0, 0.0};
+    safe_step_one<SOLVER, MODE, K, ST>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
+                                       seed, off, stamps, oc, ep_pre, ep0);
+    store_state<MODE>(x, B, i, xs);
+    st_out(&aux[i], a);
+    st_out(&step[i], st);
+    __shared__ float obs_stage[kBlock / 64][64 * D::NO];
+    store_obs32_staged<MODE>(obs_out, i, B, xs, oc, obs_stage[threadIdx.x >> 6]);
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
+    st_out(&reward[i], rew);
+    st_out(&cost[i], cst);
+    st_out(&done[i], (uint8_t)dn);
+    if (goal_met) st_out(&goal_met[i], (uint8_t)gm);
+    stamps.mark(6, false);
+    report(status, status_out, i, fail_flag);
+    stamps.mark(7, true);
+}
+
+}  // namespace rcbf

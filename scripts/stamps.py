@@ -1,12 +1,24 @@
-"""Phase timing of the fused step from a -DRCBF_STAMPS=1 diagnostic build
-(per-wave s_memtime at phase boundaries).  Usage:
-  RCBF_HIP_LIB=build/variants/librcbf_stamps.so python scripts/stamps.py [B]"""
+"""Phase timing of the fused step from the study build
+(sac-rcbf_amd/csrc/study/rcbf_stamps.hip: the same kernel template with
+per-wave s_memtime stamps at phase boundaries).  Build it here (hipcc,
+gfx950) with `python scripts/stamps.py --build`, then on the GPU:
+  python scripts/stamps.py [B] [unicycle [K]] [--eager]"""
 import ctypes
 import os
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "sac-rcbf_amd")]
+STUDY_LIB = os.path.join(ROOT, "build", "study", "librcbf_stamps.so")
+if "--build" in sys.argv:
+    os.makedirs(os.path.dirname(STUDY_LIB), exist_ok=True)
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+           "-fhip-fp32-correctly-rounded-divide-sqrt", "-I" + os.path.join(ROOT, "include"),
+           "-I" + os.path.join(ROOT, "sac-rcbf_amd", "csrc"), "-o", STUDY_LIB,
+           os.path.join(ROOT, "sac-rcbf_amd", "csrc", "study", "rcbf_stamps.hip")]
+    subprocess.run(cmd, check=True)
+    sys.exit(0)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -19,10 +31,13 @@ class A:
     cuda = True
 
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-uni = "unicycle" in sys.argv[2:]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+B = int(args[0]) if args else 65536
+uni = "unicycle" in args[1:]
 if uni:
-    hz = np.array([[0., 0.], [-1., 1.], [-1., -1.]]) * 1.5
+    k = int(args[2]) if len(args) > 2 else 3
+    from rcbf_amd.envs import _EnvSpec
+    hz = _EnvSpec("Unicycle").hazards_locations[:k]
     env = BatchedUnicycleEnv(B, seed=3, hazards_locations=hz)
 else:
     env = BatchedSimulatedCarsEnv(B, seed=3)
@@ -35,7 +50,10 @@ o = env.make_outputs()
 nw = (B + 63) // 64
 st = torch.zeros(nw * 16, dtype=torch.int64, device="cuda")
 u = (torch.rand(B, env.n_u, device="cuda") * 2 - 1).contiguous()
-lib = _lib.load()
+slib = ctypes.CDLL(STUDY_LIB)
+P = ctypes.c_void_p
+slib.rcbf_study_safe_step_stamps.argtypes = [ctypes.POINTER(_lib.RcbfParams), ctypes.c_int64] + [P] * 11 + [
+    ctypes.c_int32, ctypes.c_uint64, P]
 names = ["load", "get_state", "rows+norm", "QP", "env step", "obs+stores issued", "stores drained"]
 res = []
 fbs = []
@@ -43,10 +61,11 @@ graph = "--eager" not in sys.argv  # default: steady state inside a hipGraph rep
 
 
 def launch():
-    rc = lib.rcbf_safe_step(ctypes.byref(layer._prm), B, _lib.ptr(env.x), _lib.ptr(env.aux), _lib.ptr(env.step_count),
-                            _lib.ptr(env.episode), _lib.ptr(u), None, None, _lib.ptr(env.obs), _lib.ptr(o["u"]),
-                            _lib.ptr(o["reward"]), _lib.ptr(o["cost"]), _lib.ptr(o["done"]), None, _lib.ptr(st),
-                            None, 1, 1, 0, _lib.stream_of(torch.device("cuda")))
+    rc = slib.rcbf_study_safe_step_stamps(ctypes.byref(layer._prm), B, _lib.ptr(env.x), _lib.ptr(env.aux),
+                                          _lib.ptr(env.step_count), _lib.ptr(env.episode), _lib.ptr(u),
+                                          _lib.ptr(env.obs), _lib.ptr(o["u"]), _lib.ptr(o["reward"]),
+                                          _lib.ptr(o["cost"]), _lib.ptr(o["done"]), _lib.ptr(st), 1, 1,
+                                          _lib.stream_of(torch.device("cuda")))
     assert rc == 0
 
 
@@ -76,6 +95,6 @@ print(f"B={B} ({'hipGraph replay' if graph else 'eager'}): per-phase s_memtime t
 for k, n in enumerate(names):
     print(f"  {n:20s} {np.median(d[:, k]):8.0f} {np.percentile(d[:, k], 90):8.0f}")
 fbv = np.concatenate(fbs)
-print(f"  waves with >=1 fp64-fallback lane: {(fbv > 0).mean():.4f}; lanes: {fbv.sum() / (64 * fbv.size):.5f}")
+print(f"  lanes whose action the filter changed: {fbv.sum() / (64 * fbv.size):.4f}")
 tot = d.sum(1)
 print(f"  {'total':20s} {np.median(tot):8.0f} {np.percentile(tot, 90):8.0f}")
