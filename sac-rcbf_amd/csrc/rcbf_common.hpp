@@ -180,7 +180,7 @@ __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const floa
 #pragma unroll
         for (int k = 0; k < D::N; ++k) L.Graw[r][k] = L.G[r][k];
     }
-    normalize_rows<D::N, D::M, float>(L.G, L.h, L.Nrm, L.ish);
+    normalize_layer_rows<D::N, D::M, 2 * D::NU>(L.G, L.h, L.Nrm, L.ish);
     stamps.mark(3, false);
     PMat<D::N, true> pm;
     double pd[D::N], q[D::N];

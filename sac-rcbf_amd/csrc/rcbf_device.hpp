@@ -1357,6 +1357,31 @@ __device__ __forceinline__ void normalize_rows(T (*G)[N], T* h, T* Nrm, bool* ar
     }
 }
 
+// The same normalisation for the layer's rows, knowing their structure: the
+// last 2 n_u rows are the actuator box (one +-1 entry, zeros elsewhere,
+// diff_cbf_qp.py:362-377), so N = max(1, |h|), the unit entry becomes
+// +-RN32(1/N), the zeros stay +0 (0 / N for finite N >= 1) and h becomes
+// RN32(h / N) -- the values normalize_rows produces, without the zero
+// entries' arithmetic.  The CBF rows take the general path.
+template <int N, int M, int NBOX>
+__device__ __forceinline__ void normalize_layer_rows(float (*G)[N], float* h, float* Nrm, bool* argmax_is_h) {
+    normalize_rows<N, M - NBOX, float>(G, h, Nrm, argmax_is_h);
+#pragma unroll
+    for (int r = M - NBOX; r < M; ++r) {
+        const int c = (r - (M - NBOX)) >> 1;  // the bounded coordinate
+        const float g = G[r][c];              // +-1
+        const float ah = fabsf(h[r]);
+        const bool ish = ah > fabsf(g);
+        const float nr = ish ? ah : fabsf(g);
+        Nrm[r] = nr;
+        if (argmax_is_h) argmax_is_h[r] = ish;
+        const double rn = rcp64_nz((double)nr);
+#pragma unroll
+        for (int k = 0; k < N; ++k) G[r][k] = (k == c) ? div_f32_via_rcp(g, rn) : 0.0f;
+        h[r] = div_f32_via_rcp(h[r], rn);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // CBF constraint builders
 // ---------------------------------------------------------------------------
