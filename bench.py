@@ -262,6 +262,8 @@ def main():
         active_frac, layer = 0.0, None
         sync = lambda: None  # noqa: E731
     else:
+        if local >= torch.cuda.device_count():
+            raise SystemExit(f"rank {rank}: LOCAL_RANK {local}, but {torch.cuda.device_count()} HIP device(s) visible")
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if world > 1:
