@@ -26,11 +26,21 @@ __device__ __forceinline__ void st_out(T* p, T v) {
     __builtin_nontemporal_store(v, p);
 }
 
-// 16-byte store (staged observation chunks)
+// 16-byte store (staged observation chunks).  WT: write-through (`sc1`), the
+// line leaves the XCD's L2 as it is written instead of waiting, dirty, for the
+// kernel-end write-back.  The cars step takes it (4.40 -> 4.18 us per step,
+// rocprof-traced 5.26 -> 5.03 us; profiles/r02/obs_store_flavours_r02m.txt);
+// the unicycle step is slower with it (5.08 -> 5.41 us) and keeps `nt`.
+template <bool WT = false>
 __device__ __forceinline__ void st_out4(float* p, float4 v) {
     typedef float f4 __attribute__((ext_vector_type(4)));
-    f4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<f4*>(p));
+    const f4 w = {v.x, v.y, v.z, v.w};
+    if constexpr (WT) {
+        // the s_nop covers the store-data hazard the compiler cannot see inside the asm
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+    } else {
+        __builtin_nontemporal_store(w, reinterpret_cast<f4*>(p));
+    }
 }
 
 // 16-byte f64 pair store (env state pairs)

@@ -98,7 +98,7 @@ __device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_
 #pragma unroll
     for (int j = 0; j < (CH + 63) / 64; ++j) {
         const int c = j * 64 + lane;
-        if (CH % 64 == 0 || c < CH) st_out4(dst + 4 * c, src[c]);
+        if (CH % 64 == 0 || c < CH) st_out4<MODE == RCBF_MODE_SIMULATED_CARS>(dst + 4 * c, src[c]);
     }
 }
 
