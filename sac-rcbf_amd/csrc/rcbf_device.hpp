@@ -1098,16 +1098,22 @@ __device__ __forceinline__ void cars_qp_1d(const PMat<2, true>& pm, const R (*G)
 // (Sherman-Morrison on diag(p0,p1) + p2 a a'), the minimiser on one kink line
 // e_i = e_j, or a triple point e_i = e_j = e_l (phi is differentiable where an
 // e_j crosses 0); the argmin of phi over these candidates is exact.
+// Certificates let most waves stop after u = 0 and the pieces: phi is convex
+// and phi = max_j f_j with f_j = p0 u0^2 + p1 u1^2 + p2 max(0, e_j)^2, so
+//   * u = 0 is optimal when every b_j <= 0 (phi(0) = 0 <= phi);
+//   * piece j's stationary point u_j is optimal when e_j(u_j) > 0 and piece j
+//     attains the max there (ties included): then f_j is active at u_j and
+//     grad f_j(u_j) = 0 lies in the subdifferential of phi.
+// The kink and triple candidates run only in waves with an uncertified lane
+// (a wave-uniform ballot) and only update such lanes.
 // Stage 2: if that point u_f leaves the box, the constrained optimum lies on
 // a FACING edge -- one whose constraint u_f violates (otherwise a small step
-// from it toward u_f stays feasible and strictly lowers phi).  So one u0-edge
-// (u0 = clamp(u_f0)) and one u1-edge (u1 = clamp(u_f1)) suffice; each is a
-// 1-D problem solved exactly like cars_qp_1d (clamped stationary points and
-// kinks).  For a coordinate u_f does not violate, the "edge" is an interior
-// line whose candidates are still feasible points -- harmless -- so both
-// edges run branch-free in every lane.  (Stage 2 stays exact for the pruned
-// phi: it equals the full phi on the box, and the facing-edge argument holds
-// for any convex function.)
+// from it toward u_f stays feasible and strictly lowers phi).  So the u0-edge
+// (u0 = clamp(u_f0)) is needed only where u_f0 leaves [L0, U0], the u1-edge
+// only where u_f1 leaves [L1, U1]; each is a 1-D problem solved exactly like
+// cars_qp_1d (clamped stationary points and kinks, with stage 1's
+// certificates), run only in waves with a lane that needs it.  (Stage 2 stays exact for the pruned phi: it equals the full
+// phi on the box, and the facing-edge argument holds for any convex function.)
 template <int KK>
 __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2, double ip0, double ip1,
                                                  const double* a0, const double* a1, const double* b, double L0,
@@ -1119,99 +1125,139 @@ __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2
         for (int j = 0; j < KK; ++j) e = fmax(e, fma(a0[j], u0, fma(a1[j], u1, b[j])));
         return e;
     };
-    auto phi = [&](double u0, double u1) {
-        double e = eps_of(u0, u1);
-        return fma(p0 * u0, u0, fma(p1 * u1, u1, p2 * e * e));
+    auto phi_e = [&](double u0, double u1, double e) { return fma(p0 * u0, u0, fma(p1 * u1, u1, p2 * e * e)); };
+    bool open = true;  // no certificate yet
+    auto take = [&](double u0, double u1) {
+        double f = phi_e(u0, u1, eps_of(u0, u1));
+        bool t = open && f < bf;  // NaN candidates never win
+        bu0 = t ? u0 : bu0;
+        bu1 = t ? u1 : bu1;
+        bf = t ? f : bf;
     };
     bu0 = 0.0;
     bu1 = 0.0;
-    bf = phi(0.0, 0.0);
-    auto take = [&](double u0, double u1) {
-        double f = phi(u0, u1);
-        bool t = f < bf;  // NaN candidates never win
-        bu0 = t ? u0 : bu0;
-        bu1 = t ? u1 : bu1;
-        bf = fmin(bf, f);  // = t ? f : bf (fmin drops a NaN f)
-    };
-    // stage 1: box-free candidates
+    bool all_neg = true;
+#pragma unroll
+    for (int j = 0; j < KK; ++j) all_neg = all_neg && (b[j] <= 0.0);
+    bf = phi_e(0.0, 0.0, eps_of(0.0, 0.0));
+    open = !all_neg;
+    // stage 1a: the pieces' stationary points, with their certificates
 #pragma unroll
     for (int j = 0; j < KK; ++j) {  // piece j: (diag(p0,p1) + p2 a a') u = -p2 b a
         double w0 = a0[j] * ip0, w1 = a1[j] * ip1;
         double sden = fma(p2, fma(a0[j], w0, a1[j] * w1), 1.0);
         double f = -p2 * b[j] * rcp64_qp_nz(sden);
-        take(f * w0, f * w1);
+        const double u0 = f * w0, u1 = f * w1;
+        const double ej = fma(a0[j], u0, fma(a1[j], u1, b[j]));
+        const double em = eps_of(u0, u1);
+        const double fv = phi_e(u0, u1, em);
+        const bool cert = ej > 0.0 && ej >= em;
+        const bool t = open && (cert || fv < bf);
+        bu0 = t ? u0 : bu0;
+        bu1 = t ? u1 : bu1;
+        bf = t ? fv : bf;
+        open = open && !cert;
     }
+    // stage 1b: kinks and triple points, for the uncertified lanes
+    if (KK > 1 && __ballot(open) != 0) {
 #pragma unroll
-    for (int i = 0; i < KK; ++i) {
+        for (int i = 0; i < KK; ++i) {
 #pragma unroll
-        for (int j = i + 1; j < KK; ++j) {  // kink line (a_i - a_j).u = b_j - b_i, minimise along it
-            double d0 = a0[i] - a0[j], d1 = a1[i] - a1[j], c = b[j] - b[i];
-            // parallel pieces (dd = 0) give NaN through rcp64_qp_nz and never win
-            double dd = fma(d0, d0, d1 * d1);
-            double idd = rcp64_qp_nz(dd);
-            double q0 = c * d0 * idd, q1 = c * d1 * idd;  // a point on the line
-            double n0 = -d1, n1 = d0;                     // its direction
-            double ea = fma(a0[i], q0, fma(a1[i], q1, b[i])), an = fma(a0[i], n0, a1[i] * n1);
-            double num = fma(p0 * q0, n0, fma(p1 * q1, n1, p2 * ea * an));
-            double den = fma(p0 * n0, n0, fma(p1 * n1, n1, p2 * an * an));
-            double t = -num * rcp64_qp_nz(den);
-            take(fma(t, n0, q0), fma(t, n1, q1));
+            for (int j = i + 1; j < KK; ++j) {  // kink line (a_i - a_j).u = b_j - b_i, minimise along it
+                double d0 = a0[i] - a0[j], d1 = a1[i] - a1[j], c = b[j] - b[i];
+                // parallel pieces (dd = 0) give NaN through rcp64_qp_nz and never win
+                double dd = fma(d0, d0, d1 * d1);
+                double idd = rcp64_qp_nz(dd);
+                double q0 = c * d0 * idd, q1 = c * d1 * idd;  // a point on the line
+                double n0 = -d1, n1 = d0;                     // its direction
+                double ea = fma(a0[i], q0, fma(a1[i], q1, b[i])), an = fma(a0[i], n0, a1[i] * n1);
+                double num = fma(p0 * q0, n0, fma(p1 * q1, n1, p2 * ea * an));
+                double den = fma(p0 * n0, n0, fma(p1 * n1, n1, p2 * an * an));
+                double t = -num * rcp64_qp_nz(den);
+                take(fma(t, n0, q0), fma(t, n1, q1));
+            }
         }
-    }
 #pragma unroll
-    for (int i = 0; i < KK; ++i) {
+        for (int i = 0; i < KK; ++i) {
 #pragma unroll
-        for (int j = i + 1; j < KK; ++j) {
+            for (int j = i + 1; j < KK; ++j) {
 #pragma unroll
-            for (int l = j + 1; l < KK; ++l) {  // triple point e_i = e_j = e_l
-                double m00 = a0[i] - a0[j], m01 = a1[i] - a1[j], r0 = b[j] - b[i];
-                double m10 = a0[i] - a0[l], m11 = a1[i] - a1[l], r1 = b[l] - b[i];
-                double det = fma(m00, m11, -m01 * m10);
-                double id = rcp64_qp_nz(det);  // det = 0: NaN, never wins
-                take((r0 * m11 - r1 * m01) * id, (m00 * r1 - m10 * r0) * id);
+                for (int l = j + 1; l < KK; ++l) {  // triple point e_i = e_j = e_l
+                    double m00 = a0[i] - a0[j], m01 = a1[i] - a1[j], r0 = b[j] - b[i];
+                    double m10 = a0[i] - a0[l], m11 = a1[i] - a1[l], r1 = b[l] - b[i];
+                    double det = fma(m00, m11, -m01 * m10);
+                    double id = rcp64_qp_nz(det);  // det = 0: NaN, never wins
+                    take((r0 * m11 - r1 * m01) * id, (m00 * r1 - m10 * r0) * id);
+                }
             }
         }
     }
-    const bool inbox = (bu0 >= L0) && (bu0 <= U0) && (bu1 >= L1) && (bu1 <= U1);
-    // stage 2 (branch-free): the facing u0-edge and u1-edge
+    const bool need0 = !((bu0 >= L0) && (bu0 <= U0)), need1 = !((bu1 >= L1) && (bu1 <= U1));
+    const bool inbox = !need0 && !need1;
+    // stage 2: the facing u0-edge (u0 fixed, where u_f0 leaves [L0, U0]) and
+    // u1-edge (where u_f1 leaves [L1, U1]), each only in waves with such a lane
     const double v0 = fmin(fmax(bu0, L0), U0), v1 = fmin(fmax(bu1, L1), U1);
     bf = inbox ? bf : __builtin_huge_val();  // an out-of-box stage-1 point must not win
-    auto edge = [&](bool fix0, double v, double lo, double hi) {
+    auto edge = [&](bool fix0, double v, double lo, double hi, bool nd) {
         // free coordinate y in [lo, hi]; e_j = al_j y + be_j and
-        // phi(y) = pf y^2 + (p_fixed v^2 + p2 eps(y)^2)
+        // phi(y) = pf y^2 + (p_fixed v^2 + p2 eps(y)^2): a 1-D convex problem
+        // whose minimiser is the clamp of the unconstrained one, certified like
+        // stage 1 (origin: every be_j <= 0; piece j: e_j(y_j) > 0 is the max)
         double al[KK], be[KK];
+        bool eneg = true;
 #pragma unroll
         for (int j = 0; j < KK; ++j) {
             al[j] = fix0 ? a1[j] : a0[j];
             be[j] = fix0 ? fma(a0[j], v, b[j]) : fma(a1[j], v, b[j]);
+            eneg = eneg && (be[j] <= 0.0);
         }
         const double pf = fix0 ? p1 : p0;
         const double cfix = (fix0 ? p0 : p1) * v * v;
-        auto cand = [&](double y) {
-            y = fmin(fmax(y, lo), hi);
+        auto emax = [&](double y) {
             double e = 0.0;
 #pragma unroll
             for (int j = 0; j < KK; ++j) e = fmax(e, fma(al[j], y, be[j]));
-            const double f = fma(pf * y, y, fma(p2 * e, e, cfix));
-            const bool t = f < bf;
-            bu0 = t ? (fix0 ? v : y) : bu0;
-            bu1 = t ? (fix0 ? y : v) : bu1;
-            bf = fmin(bf, f);
+            return e;
         };
-        cand(0.0);
+        auto fval = [&](double y) {
+            const double e = emax(y);
+            return fma(pf * y, y, fma(p2 * e, e, cfix));
+        };
+        double ey = fmin(fmax(0.0, lo), hi);
+        double ef = fval(ey);
+        bool eopen = !eneg;
 #pragma unroll
-        for (int j = 0; j < KK; ++j) cand(-(p2 * al[j] * be[j]) * rcp64_qp_nz(fma(p2 * al[j], al[j], pf)));
+        for (int j = 0; j < KK; ++j) {
+            const double yr = -(p2 * al[j] * be[j]) * rcp64_qp_nz(fma(p2 * al[j], al[j], pf));
+            const double ej = fma(al[j], yr, be[j]);
+            const bool cert = ej > 0.0 && ej >= emax(yr);
+            const double y = fmin(fmax(yr, lo), hi);
+            const double f = fval(y);
+            const bool t = eopen && (cert || f < ef);
+            ey = t ? y : ey;
+            ef = t ? f : ef;
+            eopen = eopen && !cert;
+        }
+        if (KK > 1 && __ballot(nd && eopen) != 0) {
 #pragma unroll
-        for (int i = 0; i < KK; ++i)
+            for (int i = 0; i < KK; ++i)
 #pragma unroll
-            for (int j = i + 1; j < KK; ++j) {
-                // den = 0: NaN, which the clamp in cand turns into the feasible point lo
-                double den = al[i] - al[j];
-                cand((be[j] - be[i]) * rcp64_qp_nz(den));
-            }
+                for (int j = i + 1; j < KK; ++j) {
+                    // den = 0: NaN, which the clamp turns into the feasible point lo
+                    const double y = fmin(fmax((be[j] - be[i]) * rcp64_qp_nz(al[i] - al[j]), lo), hi);
+                    const double f = fval(y);
+                    const bool t = eopen && f < ef;
+                    ey = t ? y : ey;
+                    ef = t ? f : ef;
+                }
+        }
+        const bool t = nd && ef < bf;
+        bu0 = t ? (fix0 ? v : ey) : bu0;
+        bu1 = t ? (fix0 ? ey : v) : bu1;
+        bf = t ? ef : bf;
     };
-    edge(true, v0, L1, U1);
-    edge(false, v1, L0, U0);
+    if (__ballot(need0) != 0) edge(true, v0, L1, U1, need0);
+    if (__ballot(need1) != 0) edge(false, v1, L0, U0, need1);
 }
 
 // Wave-uniform maximum of a small per-lane count (0..K).

@@ -3,8 +3,9 @@
 # abort, segfault or time-out ends the session (no further GPU step).
 # Usage: bash scripts/gpu_session.sh TAG step [step ...]
 #   steps: smoke | pytest | bench | benchx
-#          prof_<w> | pmc_<w> | sq_<w>    with workload <w> = cars | uni3 | uni5
-#          (rocprofv3 kernel-trace stats; FETCH_SIZE and WRITE_SIZE passes;
+#          b_<w> | prof_<w> | pmc_<w> | sq_<w>    with workload <w> = cars | uni3 | uni5
+#          (bench.py without the CPU baseline;
+#           rocprofv3 kernel-trace stats; FETCH_SIZE and WRITE_SIZE passes;
 #           SQ instruction counts -- each counter pass its own run)
 set -u
 TAG=${1:?tag}; shift
@@ -46,6 +47,7 @@ for step in "$@"; do
     pytest) run pytest 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;
     benchx) run benchx 600 python bench.py --extra --no-cpu-baseline ;;
+    b_*)    run "b_$wl" 300 python bench.py --no-cpu-baseline $(wl_args "$wl") ;;
     prof_*)
       run "prof_$wl" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$wl" -o run -- \
         python3 bench.py --no-cpu-baseline $(wl_args "$wl")

@@ -51,13 +51,15 @@ def cars_qp_1d(Gn, hn, pd):
     return np.stack([u, eps(u)], 1)
 
 
-def uni_qp_2d(Gn, hn, pd, K, prune=True, wave=64):
+def uni_qp_2d(Gn, hn, pd, K, prune=True, wave=64, stats=None):
     """Unicycle QP: variables (u0, u1, eps), rows [K cbf rows, 4 box rows].
     Pruning (as the kernel): per lane, only the rows whose a_j.u + b_j can
     exceed 0 somewhere in the box are kept, compacted into slots (unused
     slots repeat slot 0); lanes are grouped in waves of `wave` and each wave
     solves with KK = its largest live count (KK = 0: the clamped origin).
-    Returns ((B,3) z, in-box mask of the stage-1 point, KK per lane)."""
+    Returns ((B,3) z, in-box mask of the stage-1 point, KK per lane); `stats`
+    (a dict) receives per-lane `open` (no certificate after the pieces:
+    the lane's wave runs the kink / triple stage)."""
     G = Gn.astype(np.float64)
     h = hn.astype(np.float64)
     B = G.shape[0]
@@ -70,7 +72,9 @@ def uni_qp_2d(Gn, hn, pd, K, prune=True, wave=64):
     U1 = h[:, K + 2] / G[:, K + 2, 1]
     L1 = h[:, K + 3] / G[:, K + 3, 1]
     if not prune:
-        z, inb = _pieces_solve(a0, a1, b, L0, U0, L1, U1, pd)
+        z, inb, opn = _pieces_solve(a0, a1, b, L0, U0, L1, U1, pd, stats)
+        if stats is not None:
+            stats["open"] = opn
         return _with_eps(z, a0, a1, b), inb, np.full(B, K)
     emax = b + np.maximum(a0 * L0[:, None], a0 * U0[:, None]) + np.maximum(a1 * L1[:, None], a1 * U1[:, None])
     live = ~(emax <= 0)
@@ -90,6 +94,8 @@ def uni_qp_2d(Gn, hn, pd, K, prune=True, wave=64):
     kk = np.repeat(kk.reshape(nw, wave).max(1), wave)[:B]
     z = np.zeros((B, 2))
     inb = np.ones(B, bool)
+    opn = np.zeros(B, bool)
+    st = {k: np.zeros(B, bool) for k in ("need_u0_edge", "need_u1_edge", "edge_open")}
     for KK in range(K + 1):
         r = np.nonzero(kk == KK)[0]
         if r.size == 0:
@@ -98,8 +104,14 @@ def uni_qp_2d(Gn, hn, pd, K, prune=True, wave=64):
             z[r, 0] = np.minimum(np.maximum(0.0, L0[r]), U0[r])
             z[r, 1] = np.minimum(np.maximum(0.0, L1[r]), U1[r])
             continue
-        zr, ir = _pieces_solve(A0[r, :KK], A1[r, :KK], Bv[r, :KK], L0[r], U0[r], L1[r], U1[r], pd)
-        z[r], inb[r] = zr, ir
+        sr = {}
+        zr, ir, orr = _pieces_solve(A0[r, :KK], A1[r, :KK], Bv[r, :KK], L0[r], U0[r], L1[r], U1[r], pd, sr)
+        z[r], inb[r], opn[r] = zr, ir, orr
+        for k in st:
+            st[k][r] = sr[k]
+    if stats is not None:
+        stats["open"] = opn
+        stats.update(st)
     return _with_eps(z, a0, a1, b), inb, kk
 
 
@@ -108,8 +120,12 @@ def _with_eps(z, a0, a1, b):
     return np.concatenate([z, e[:, None]], 1)
 
 
-def _pieces_solve(a0, a1, b, L0, U0, L1, U1, pd):
-    """Stage 1 + stage 2 of the kernel's uni_pieces_solve on K pieces."""
+def _pieces_solve(a0, a1, b, L0, U0, L1, U1, pd, stats=None):
+    """Stage 1 + stage 2 of the kernel's uni_pieces_solve on K pieces.  A
+    lane whose origin (every b_j <= 0) or piece stationary point u_j (e_j(u_j)
+    > 0 and piece j attains the max there) is certified takes that point (the
+    first certified one); the others take the argmin over all candidates.
+    Returns (z, in-box mask, open mask)."""
     p0, p1, p2 = pd
     B, K = a0.shape
 
@@ -121,12 +137,16 @@ def _pieces_solve(a0, a1, b, L0, U0, L1, U1, pd):
         return p0 * u0 * u0 + p1 * u1 * u1 + p2 * e * e
 
     C = [(np.zeros(B), np.zeros(B))]
+    cert_k = np.where((b <= 0).all(1), 0, -1)  # index into C of the certified candidate, -1: none
     for j in range(K):
         w0 = a0[:, j] / p0
         w1 = a1[:, j] / p1
         s = 1 + p2 * (a0[:, j] * w0 + a1[:, j] * w1)
         f = -p2 * b[:, j] / s
         C.append((f * w0, f * w1))
+        ej = a0[:, j] * C[-1][0] + a1[:, j] * C[-1][1] + b[:, j]
+        cj = (ej > 0) & (ej >= eps(*C[-1]))
+        cert_k = np.where((cert_k < 0) & cj, len(C) - 1, cert_k)
     for i in range(K):
         for j in range(i + 1, K):
             d0 = a0[:, i] - a0[:, j]
@@ -155,30 +175,46 @@ def _pieces_solve(a0, a1, b, L0, U0, L1, U1, pd):
         det = np.where(ok, det, 1)
         C.append((np.where(ok, (r0 * m11 - r1 * m01) / det, 0), np.where(ok, (m00 * r1 - m10 * r0) / det, 0)))
     Fv = np.stack([phi(u0, u1) for u0, u1 in C], 1)
-    k = np.nanargmin(Fv, 1)
+    k = np.where(cert_k >= 0, cert_k, np.nanargmin(Fv, 1))
     U0s = np.stack([c[0] for c in C], 1)[np.arange(B), k]
     U1s = np.stack([c[1] for c in C], 1)[np.arange(B), k]
     inb = (U0s >= L0) & (U0s <= U0) & (U1s >= L1) & (U1s <= U1)
+    # stage 2: the facing edges of the out-of-box lanes -- the u0-edge (u0 fixed
+    # at clamp(u_f0)) only where u_f0 leaves [L0, U0], the u1-edge only where
+    # u_f1 leaves [L1, U1]; on each edge the origin / piece certificates as in
+    # stage 1, else the argmin over the edge's candidates
     best = np.full(B, np.inf)
     bu0, bu1 = U0s.copy(), U1s.copy()
     v0 = np.minimum(np.maximum(U0s, L0), U0)
     v1 = np.minimum(np.maximum(U1s, L1), U1)
-    for fix0, v, lo, hi in [(True, v0, L1, U1), (False, v1, L0, U0)]:
+    need = [(U0s < L0) | (U0s > U0), (U1s < L1) | (U1s > U1)]
+    edge_open = np.zeros(B, bool)
+    for fix0, v, lo, hi, nd in [(True, v0, L1, U1, need[0]), (False, v1, L0, U0, need[1])]:
         al = a1 if fix0 else a0
         be = (a0 * v[:, None] + b) if fix0 else (a1 * v[:, None] + b)
         pf = p1 if fix0 else p0
         ys = [np.zeros(B)] + [-(p2 * al[:, j] * be[:, j]) / (p2 * al[:, j] ** 2 + pf) for j in range(K)]
+        ecert = np.where((be <= 0).all(1), 0, -1)
+        for j in range(K):
+            ej = al[:, j] * ys[j + 1] + be[:, j]
+            em = np.maximum(0, (al * ys[j + 1][:, None] + be).max(1))
+            ecert = np.where((ecert < 0) & (ej > 0) & (ej >= em), j + 1, ecert)
         for i in range(K):
             for j in range(i + 1, K):
                 den = al[:, i] - al[:, j]
                 ys.append(np.where(den != 0, (be[:, j] - be[:, i]) / np.where(den != 0, den, 1), 0))
-        for y in ys:
-            y = np.minimum(np.maximum(y, lo), hi)
-            u0 = v if fix0 else y
-            u1 = y if fix0 else v
-            f = phi(u0, u1)
-            t = (f < best) & ~inb
-            best = np.where(t, f, best)
-            bu0 = np.where(t, u0, bu0)
-            bu1 = np.where(t, u1, bu1)
-    return np.stack([bu0, bu1], 1), inb
+        edge_open |= nd & (ecert < 0)
+        Y = np.stack([np.minimum(np.maximum(y, lo), hi) for y in ys], 1)
+        Fe = np.stack([phi(v, Y[:, k]) if fix0 else phi(Y[:, k], v) for k in range(Y.shape[1])], 1)
+        ke = np.where(ecert >= 0, ecert, np.nanargmin(np.where(np.isnan(Fe), np.inf, Fe), 1))
+        y = Y[np.arange(B), ke]
+        f = Fe[np.arange(B), ke]
+        u0 = v if fix0 else y
+        u1 = y if fix0 else v
+        t = nd & (f < best)
+        best = np.where(t, f, best)
+        bu0 = np.where(t, u0, bu0)
+        bu1 = np.where(t, u1, bu1)
+    if stats is not None:
+        stats["need_u0_edge"], stats["need_u1_edge"], stats["edge_open"] = need[0], need[1], edge_open
+    return np.stack([bu0, bu1], 1), inb, cert_k < 0

@@ -123,12 +123,17 @@ def test_uni_pruning_on_the_bench_distribution(K):
     Gn, hn, _ = O.normalize_rows(G, h)
     pd = np.array([np.float64(F(1.0)), np.float64(F(1e-2)), np.float64(F(1e5))])
     z, lam, act, st = O.qp_exact(pd, Gn, hn)
-    z2, _, kk = uni_qp_2d(Gn, hn, pd, K)
+    stats = {}
+    z2, inb, kk = uni_qp_2d(Gn, hn, pd, K, stats=stats)
     ok = st == 0
     err = np.abs(z2 - z).max(1) / np.maximum(1, np.abs(z).max(1))
     assert err[ok].max() < 1e-6
     waves = kk[::64]
     assert (waves <= 2).mean() > 0.9, np.bincount(waves)
+    # the certificates: what fraction of waves runs each optional stage
+    w = {k: stats[k].reshape(-1, 64).any(1).mean() for k in ("open", "need_u0_edge", "need_u1_edge", "edge_open")}
+    print(K, w, (~inb).reshape(-1, 64).any(1).mean())
+    assert w["open"] < 0.5 and w["edge_open"] < 0.5, w
 
 
 def _fma(a, b, c):
