@@ -537,7 +537,7 @@ def generic_qp_rows(layer, dev):
                 lib.rcbf_qp_backward(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(gz),
                                      _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh), _lib.stream_of(dev))
             by_in = 4 * (n * n + n + m * n + m)
-            fms, bms = _time_graph(fwd, 20, dev), _time_graph(bwd, 20, dev)
+            fms, bms = _time_graph(fwd, 200, dev), _time_graph(bwd, 200, dev)
             out[f"qp_n{n}_m{m}_B{B}"] = {
                 "fwd_us": round(fms * 1e3, 2), "bwd_us": round(bms * 1e3, 2),
                 "fwd_GBs": round(B * (by_in + 4 * n) / fms / 1e6, 1),
@@ -576,7 +576,7 @@ def generic_qp_rows(layer, dev):
         def bwd_l():
             lib.rcbf_qp_backward(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(gz),
                                  _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh), _lib.stream_of(dev))
-        fms, bms = _time_graph(fwd_l, 20, dev), _time_graph(bwd_l, 20, dev)
+        fms, bms = _time_graph(fwd_l, 200, dev), _time_graph(bwd_l, 200, dev)
         by_in = 4 * (n * n + n + m * n + m)
         out[f"qp_layer_rows_{name}_B{B}"] = {"fwd_us": round(fms * 1e3, 2), "bwd_us": round(bms * 1e3, 2),
                                              "fwd_GBs": round(B * (by_in + 4 * n) / fms / 1e6, 1),

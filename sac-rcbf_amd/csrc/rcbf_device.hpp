@@ -218,7 +218,18 @@ __device__ __forceinline__ void pmat_set_diag(PMat<N, true>& pm, const double* d
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         pm.P[i][i] = d[i];
-        pm.Pinv[i][i] = 1.0 / d[i];
+        pm.Pinv[i][i] = 1.0 / d[i];  // compile-time constants in the fused kernels: folded
+    }
+}
+
+// the same for a run-time diagonal (the generic QP kernels): one reciprocal
+// instead of an IEEE division sequence each
+template <int N>
+__device__ __forceinline__ void pmat_set_diag_rt(PMat<N, true>& pm, const double* d) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        pm.P[i][i] = d[i];
+        pm.Pinv[i][i] = rcp64(d[i]);
     }
 }
 
@@ -639,7 +650,7 @@ __device__ __forceinline__ void pdipm_solve(const PMat<N, DIAG>& pm, const doubl
         // normal-equation matrix H = P + G' D G
         double d[M], H[N][N];
 #pragma unroll
-        for (int r = 0; r < M; ++r) d[r] = lam[r] / s[r];
+        for (int r = 0; r < M; ++r) d[r] = lam[r] * rcp64(s[r]);
 #pragma unroll
         for (int i = 0; i < N; ++i)
 #pragma unroll
@@ -680,13 +691,13 @@ __device__ __forceinline__ void pdipm_solve(const PMat<N, DIAG>& pm, const doubl
         double a_aff = 1.0;
 #pragma unroll
         for (int r = 0; r < M; ++r) {
-            if (dl[r] < 0.0) a_aff = fmin(a_aff, -lam[r] / dl[r]);
-            if (ds[r] < 0.0) a_aff = fmin(a_aff, -s[r] / ds[r]);
+            if (dl[r] < 0.0) a_aff = fmin(a_aff, -lam[r] * rcp64(dl[r]));
+            if (ds[r] < 0.0) a_aff = fmin(a_aff, -s[r] * rcp64(ds[r]));
         }
         double t3 = 0.0;
 #pragma unroll
         for (int r = 0; r < M; ++r) t3 += (s[r] + a_aff * ds[r]) * (lam[r] + a_aff * dl[r]);
-        double sig = t3 / sz;
+        double sig = t3 * rcp64(sz);
         sig = sig * sig * sig;
         // corrector: rs = (-mu sig + ds_aff dl_aff) / s, rx = rz = 0, added
         double dxc[N], dsc[M], dlc[M];
@@ -701,7 +712,7 @@ __device__ __forceinline__ void pdipm_solve(const PMat<N, DIAG>& pm, const doubl
             for (int r = 0; r < M; ++r) {
                 rz0[r] = rz[r];
                 rz[r] = 0.0;
-                rs[r] = (-mu * sig + ds[r] * dl[r]) / s[r];
+                rs[r] = (-mu * sig + ds[r] * dl[r]) * rcp64(s[r]);
             }
             kkt(rs, dxc, dsc, dlc);
 #pragma unroll
@@ -720,8 +731,8 @@ __device__ __forceinline__ void pdipm_solve(const PMat<N, DIAG>& pm, const doubl
         double amax = kInf;
 #pragma unroll
         for (int r = 0; r < M; ++r) {
-            if (dl[r] < 0.0) amax = fmin(amax, -lam[r] / dl[r]);
-            if (ds[r] < 0.0) amax = fmin(amax, -s[r] / ds[r]);
+            if (dl[r] < 0.0) amax = fmin(amax, -lam[r] * rcp64(dl[r]));
+            if (ds[r] < 0.0) amax = fmin(amax, -s[r] * rcp64(ds[r]));
         }
         // qpth's get_step: no blocking direction -> step 1 (then x0.999)
         if (amax == kInf) amax = 1.0;

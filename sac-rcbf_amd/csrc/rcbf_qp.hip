@@ -23,11 +23,50 @@ constexpr int kQPBlock = 128;
 __host__ __device__ inline int odd_stride(int w) { return w | 1; }
 
 // LDS <- the workgroup's chunk of an AoS tensor with W <= MAXW elements per
-// QP: every lane first issues all of its (coalesced, predicated) loads, then
-// writes them to LDS, so the loads are in flight together.
+// QP, at row stride odd_stride(W) words in LDS: every lane first issues all of
+// its (coalesced, predicated) loads, then writes them to LDS, so the loads are
+// in flight together.  fp32 chunks that start 16-B aligned move as float4:
+// for odd W the padded layout IS the linear one (one ds_write_b128 per
+// float4); for even W each element lands at e + e / W (the row's pad word).
 template <typename T, int MAXW>
 __device__ __forceinline__ void stage_in(const T* __restrict__ src, T* lds, int nb, int W) {
     const int Wp = odd_stride(W), tot = nb * W;
+    if constexpr (sizeof(T) == 4) {
+        if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+            constexpr int J4 = (MAXW + 3) / 4;  // float4s per lane at a full chunk
+            const int n4 = tot >> 2;
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            f4 v[J4];
+#pragma unroll
+            for (int j = 0; j < J4; ++j) {
+                const int c4 = threadIdx.x + j * kQPBlock;
+                v[j] = c4 < n4 ? __builtin_nontemporal_load(reinterpret_cast<const f4*>(src) + c4) : f4{0, 0, 0, 0};
+            }
+            const int rem = tot - 4 * n4;  // < 4 trailing words
+            const T tail = threadIdx.x < rem ? ld_in(src + 4 * n4 + threadIdx.x) : T(0);
+            if (W & 1) {
+#pragma unroll
+                for (int j = 0; j < J4; ++j) {
+                    const int c4 = threadIdx.x + j * kQPBlock;
+                    if (c4 < n4) *reinterpret_cast<f4*>(lds + 4 * c4) = v[j];
+                }
+                if (threadIdx.x < rem) lds[4 * n4 + threadIdx.x] = tail;
+            } else {
+                const float invW = 1.0f / (float)W;  // e / W exact below 2^16 (e + 0.5 keeps off the integers)
+                auto put = [&](int e, T x) { lds[e + (int)(((float)e + 0.5f) * invW)] = x; };
+#pragma unroll
+                for (int j = 0; j < J4; ++j) {
+                    const int c4 = threadIdx.x + j * kQPBlock;
+                    if (c4 < n4) {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) put(4 * c4 + t, v[j][t]);
+                    }
+                }
+                if (threadIdx.x < rem) put(4 * n4 + threadIdx.x, tail);
+            }
+            return;
+        }
+    }
     const int e0 = threadIdx.x, q0 = e0 / W, c0 = e0 - q0 * W;
     const int dq = kQPBlock / W, dc = kQPBlock - dq * W;
     T v[MAXW];
@@ -49,10 +88,30 @@ __device__ __forceinline__ void stage_in(const T* __restrict__ src, T* lds, int 
     }
 }
 
-// the workgroup's chunk of an AoS output tensor <- LDS
+// the workgroup's chunk of an AoS output tensor <- LDS (the same two forms)
 template <typename T>
 __device__ __forceinline__ void stage_out(T* __restrict__ dst, const T* lds, int nb, int W) {
     const int Wp = odd_stride(W), tot = nb * W;
+    if constexpr (sizeof(T) == 4) {
+        if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            const int n4 = tot >> 2, rem = tot - 4 * n4;
+            const float invW = 1.0f / (float)W;
+            auto get = [&](int e) { return (W & 1) ? lds[e] : lds[e + (int)(((float)e + 0.5f) * invW)]; };
+            for (int c4 = threadIdx.x; c4 < n4; c4 += kQPBlock) {
+                f4 v;
+                if (W & 1) {
+                    v = *reinterpret_cast<const f4*>(lds + 4 * c4);
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) v[t] = get(4 * c4 + t);
+                }
+                __builtin_nontemporal_store(v, reinterpret_cast<f4*>(dst) + c4);
+            }
+            if (threadIdx.x < rem) dst[4 * n4 + threadIdx.x] = get(4 * n4 + threadIdx.x);
+            return;
+        }
+    }
     int e = threadIdx.x, q = e / W, c = e - q * W;
     const int dq = kQPBlock / W, dc = kQPBlock - dq * W;
     for (; e < tot; e += kQPBlock) {
@@ -144,7 +203,7 @@ __device__ __forceinline__ void structured_solve(const StagedQP<N, MP, T>& Q, in
     double pd[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) pd[k] = Q.P[k][k];
-    pmat_set_diag<N>(pm, pd);
+    pmat_set_diag_rt<N>(pm, pd);
     if constexpr (N == 2 && MP >= 4) {
         cars_qp_1d<T>(pm, Q.G, Q.h, z, status);
     } else if constexpr (N == 3) {
@@ -186,7 +245,7 @@ __device__ __forceinline__ bool gi_solve_chol(const StagedQP<N, MP, T>& Q, int m
             if (a == b) {
                 spd = spd && acc > 0.0;
                 L[a][a] = sqrt(acc);
-                id[a] = 1.0 / L[a][a];
+                id[a] = rcp64(L[a][a]);
             } else {
                 L[a][b] = acc * id[b];
             }
@@ -243,7 +302,7 @@ template <int N, int MP, typename T>
 __device__ __forceinline__ bool structured_multipliers(const StagedQP<N, MP, T>& Q, int m, QPResult<N, MP>& res) {
     double GA[N][N], ip[N];
 #pragma unroll
-    for (int k = 0; k < N; ++k) ip[k] = 1.0 / Q.P[k][k];
+    for (int k = 0; k < N; ++k) ip[k] = rcp64(Q.P[k][k]);
     int nact = 0, aidx[N];
     uint32_t amask = 0;
     bool ok = true;
@@ -354,7 +413,7 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_solve(rcbf_params prm, int64_t 
             double pd[N];
 #pragma unroll
             for (int k = 0; k < N; ++k) pd[k] = Q.P[k][k];
-            pmat_set_diag<N>(pm, pd);
+            pmat_set_diag_rt<N>(pm, pd);
             qp_solve<SOLVER, N, MP, true, T>(pm, Q.q, Q.G, Q.h, prm.max_iter, prm.eps, res);
         } else {
             bool done = false;
@@ -507,7 +566,7 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_bwd(rcbf_params prm, int64_t B,
         double pd[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) pd[k] = active ? Q.P[k][k] : 1.0;
-        pmat_set_diag<N>(pm, pd);
+        pmat_set_diag_rt<N>(pm, pd);
         // the layer's own rows: closed-form optimum, multipliers from stationarity (wave-uniform)
         bool fast = false;
         if (__ballot(active && !layer_structured<N, MP, float>(Q, m)) == 0) {
@@ -549,20 +608,20 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_bwd(rcbf_params prm, int64_t B,
             double gGn[N], ghn = -er;
 #pragma unroll
             for (int k = 0; k < N; ++k) gGn[k] = er * z[k] + res.lam[r] * dz[k];
-            double dN = 0.0, nr = 1.0;
+            double dN = 0.0, inr = 1.0;  // inr = 1 / N_r (one reciprocal per row)
             if (normalize) {
-                nr = (double)Nrm[r];
+                inr = rcp64((double)Nrm[r]);
                 double acc = ghn * (double)Q.h[r];
 #pragma unroll
                 for (int k = 0; k < N; ++k) acc += gGn[k] * (double)Q.G[r][k];
-                dN = -acc / nr;
+                dN = -acc * inr;
             }
             auto sgn = [](float v) { return v > 0.0f ? 1.0 : (v < 0.0f ? -1.0 : 0.0); };
 #pragma unroll
             for (int k = 0; k < N; ++k)
                 sG[lane * wg + r * N + k] =
-                    (float)(gGn[k] / nr + ((normalize && amax[r] == k) ? dN * sgn(Q.G[r][k]) : 0.0));
-            sh[lane * wh + r] = (float)(ghn / nr + ((normalize && amax[r] == N) ? dN * sgn(Q.h[r]) : 0.0));
+                    (float)(gGn[k] * inr + ((normalize && amax[r] == k) ? dN * sgn(Q.G[r][k]) : 0.0));
+            sh[lane * wh + r] = (float)(ghn * inr + ((normalize && amax[r] == N) ? dN * sgn(Q.h[r]) : 0.0));
         }
     }
     __syncthreads();
