@@ -119,6 +119,56 @@ __device__ __forceinline__ bool ldl_solve(double S[N][N], const double* w, doubl
     return ok;
 }
 
+// The same LDL^T factorisation applied to two right-hand sides.
+template <int N>
+__device__ __forceinline__ bool ldl_solve2(double S[N][N], const double* w1, const double* w2, double* r1,
+                                           double* r2) {
+    double L[N][N];
+    double D[N], Dinv[N];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        double d = S[j][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k] * D[k];
+        ok = ok && (d > 0.0);
+        D[j] = d;
+        double inv = rcp64(d);
+        Dinv[j] = inv;
+#pragma unroll
+        for (int i = j + 1; i < N; ++i) {
+            double v = S[i][j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k] * D[k];
+            L[i][j] = v * inv;
+        }
+    }
+    double y1[N], y2[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        double v1 = w1[i], v2 = w2[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) {
+            v1 -= L[i][k] * y1[k];
+            v2 -= L[i][k] * y2[k];
+        }
+        y1[i] = v1;
+        y2[i] = v2;
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        double v1 = y1[i] * Dinv[i], v2 = y2[i] * Dinv[i];
+#pragma unroll
+        for (int k = i + 1; k < N; ++k) {
+            v1 -= L[k][i] * r1[k];
+            v2 -= L[k][i] * r2[k];
+        }
+        r1[i] = v1;
+        r2[i] = v2;
+    }
+    return ok;
+}
+
 // Solve A x = b (N x N general, rows of A = active constraint normals) by
 // Gaussian elimination with partial pivoting, fully unrolled.
 template <int N>
@@ -1388,7 +1438,7 @@ __device__ __forceinline__ void qp_solve(const PMat<N, DIAG>& pm, const double* 
 // routes dN/dh only through that entry.
 // ---------------------------------------------------------------------------
 template <int N, int M, typename T>
-__device__ __forceinline__ void normalize_rows(T (*G)[N], T* h, T* Nrm, bool* argmax_is_h) {
+__device__ __forceinline__ void normalize_rows(T (*G)[N], T* h, T* Nrm, bool* argmax_is_h, double* rinv = nullptr) {
 #pragma unroll
     for (int r = 0; r < M; ++r) {
         T mx = fabs(G[r][0]);
@@ -1403,6 +1453,7 @@ __device__ __forceinline__ void normalize_rows(T (*G)[N], T* h, T* Nrm, bool* ar
             // one reciprocal per row, exact fp32 quotients; nr = 0 only for an
             // all-zero row, whose quotients are NaN either way (0 * inf, 0 * NaN)
             const double rn = rcp64_nz((double)nr);
+            if (rinv) rinv[r] = rn;
 #pragma unroll
             for (int k = 0; k < N; ++k) G[r][k] = div_f32_via_rcp(G[r][k], rn);
             h[r] = div_f32_via_rcp(h[r], rn);

@@ -367,6 +367,94 @@ __device__ __forceinline__ bool structured_multipliers(const StagedQP<N, MP, T>&
     return ok;
 }
 
+// The backward of a layer-structured QP at its closed-form optimum z
+// (diagonal P, q = 0) from ONE factorisation: the tight rows A (as
+// structured_multipliers), S = G_A P^-1 G_A' (LDL^T), then
+//   lam_A = S^-1 (-G_A z)               (stationarity P z + G_A' lam_A = 0)
+//   eta   = S^-1 (-G_A P^-1 g),  dz = -P^-1 (g + G_A' eta)   (qp_adjoint)
+// -- at a vertex (|A| = n) this is eta = -G_A'^-1 g, dz = 0.  Returns false
+// where structured_multipliers would (the caller then runs Goldfarb-Idnani and
+// qp_adjoint).
+template <int N, int MP, typename T>
+__device__ __forceinline__ bool structured_kkt_adjoint(const StagedQP<N, MP, T>& Q, int m, const double* g,
+                                                       QPResult<N, MP>& res, double* dz, double* eta, int* aidx) {
+    double GA[N][N], ip[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) ip[k] = rcp64(Q.P[k][k]);
+    int nact = 0;
+    uint32_t amask = 0;
+    bool ok = true;
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) {
+        aidx[sl] = -1;
+#pragma unroll
+        for (int k = 0; k < N; ++k) GA[sl][k] = 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < MP; ++r) {
+        double v = -(double)Q.h[r];
+#pragma unroll
+        for (int k = 0; k < N; ++k) v = fma((double)Q.G[r][k], res.z[k], v);
+        const bool tight = (r < m) && fabs(v) <= 1e-9 * (1.0 + fabs((double)Q.h[r]));
+        ok = ok && !(tight && nact >= N);
+        const bool a = tight && nact < N;
+#pragma unroll
+        for (int sl = 0; sl < N && sl <= r; ++sl) {  // row r can only land in slots 0..r
+            const bool here = a && (sl == nact);
+#pragma unroll
+            for (int k = 0; k < N; ++k) GA[sl][k] = here ? (double)Q.G[r][k] : GA[sl][k];
+            aidx[sl] = here ? r : aidx[sl];
+        }
+        amask |= a ? (1u << r) : 0u;
+        nact += a ? 1 : 0;
+    }
+    double S[N][N], w1[N], w2[N], lam[N], Pg[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) Pg[k] = ip[k] * g[k];
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+#pragma unroll
+        for (int b = 0; b <= a; ++b) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc = fma(GA[a][k] * ip[k], GA[b][k], acc);
+            S[a][b] = (a < nact && b < nact) ? acc : (a == b ? 1.0 : 0.0);
+            S[b][a] = S[a][b];
+        }
+        w1[a] = (a < nact) ? -dotd<N>(GA[a], res.z) : 0.0;
+        w2[a] = (a < nact) ? -dotd<N>(GA[a], Pg) : 0.0;
+    }
+    ok = ok && ldl_solve2<N>(S, w1, w2, lam, eta);
+    double scale = 1.0;
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) scale = fmax(scale, fabs(lam[sl]));
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) ok = ok && (sl >= nact || lam[sl] >= -1e-9 * scale);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {  // stationarity: P z + G_A' lam = 0;  dz = -P^-1 (g + G_A' eta)
+        double acc = Q.P[k][k] * res.z[k], t = g[k];
+#pragma unroll
+        for (int sl = 0; sl < N; ++sl) {
+            acc = fma((sl < nact) ? GA[sl][k] : 0.0, lam[sl], acc);
+            t = fma((sl < nact) ? GA[sl][k] : 0.0, eta[sl], t);
+        }
+        ok = ok && fabs(acc) <= 1e-7 * scale * (1.0 + fabs(Q.P[k][k] * res.z[k]));
+        dz[k] = -ip[k] * t;
+    }
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) eta[sl] = (sl < nact) ? eta[sl] : 0.0;
+#pragma unroll
+    for (int r = 0; r < MP; ++r) {
+        double l = 0.0;
+#pragma unroll
+        for (int sl = 0; sl < N; ++sl) l = (sl < nact && aidx[sl] == r) ? fmax(lam[sl], 0.0) : l;
+        res.lam[r] = l;
+    }
+    res.active = amask;
+    res.nact = nact;
+    return ok;
+}
+
 // Generic QP: rows padded to MP with the never-active row (0 z <= 1); SPD P
 // (n <= 3).  T = float: the fp32 rows of the diff layer (z returned as fp32,
 // the reference's .float()); T = double: fp64 throughout.  Per wave: the
@@ -536,6 +624,7 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_bwd(rcbf_params prm, int64_t B,
     const int64_t i = i0 + lane;
     StagedQP<N, MP, float> Q;
     float Nrm[MP];
+    double rinv[MP];  // 1 / N_r from the normaliser
     int amax[MP];
     double g[N], z[N], dz[N], eta[N];
     int aidx[N];
@@ -555,7 +644,7 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_bwd(rcbf_params prm, int64_t B,
             amax[r] = (fabsf(Q.h[r]) > mx) ? N : a;
             Nrm[r] = 1.0f;
         }
-        if (normalize) normalize_rows<N, MP, float>(Q.G, Q.h, Nrm, nullptr);
+        if (normalize) normalize_rows<N, MP, float>(Q.G, Q.h, Nrm, nullptr, rinv);
 #pragma unroll
         for (int a = 0; a < N; ++a) g[a] = (double)grad_z[i * N + a];
     } else {
@@ -573,12 +662,12 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_bwd(rcbf_params prm, int64_t B,
             bool ok = true;
             if (active) {
                 structured_solve<N, MP, float>(Q, m, res.z, res.status);
-                ok = res.status == RCBF_QP_OK && structured_multipliers<N, MP, float>(Q, m, res);
+                ok = res.status == RCBF_QP_OK && structured_kkt_adjoint<N, MP, float>(Q, m, g, res, dz, eta, aidx);
             }
             fast = __ballot(!ok) == 0;
         }
-        if (active) {
-            if (!fast) gi_solve<N, MP, true, float>(pm, Q.q, Q.G, Q.h, 4 * (MP + N) + 8, res);
+        if (active && !fast) {
+            gi_solve<N, MP, true, float>(pm, Q.q, Q.G, Q.h, 4 * (MP + N) + 8, res);
             qp_adjoint<N, MP, true>(pm, Q, g, res, dz, eta, aidx);
         }
     } else if (active) {
@@ -608,9 +697,9 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_bwd(rcbf_params prm, int64_t B,
             double gGn[N], ghn = -er;
 #pragma unroll
             for (int k = 0; k < N; ++k) gGn[k] = er * z[k] + res.lam[r] * dz[k];
-            double dN = 0.0, inr = 1.0;  // inr = 1 / N_r (one reciprocal per row)
+            double dN = 0.0, inr = 1.0;  // inr = 1 / N_r
             if (normalize) {
-                inr = rcp64((double)Nrm[r]);
+                inr = rinv[r];
                 double acc = ghn * (double)Q.h[r];
 #pragma unroll
                 for (int k = 0; k < N; ++k) acc += gGn[k] * (double)Q.G[r][k];
