@@ -281,6 +281,7 @@ def main():
         ev0.record()
     for _ in range(reps):
         graph.replay()
+    t_sub = time.perf_counter() - t0
     if not args.cpu_dry_run:
         ev1.record()
     sync()
@@ -326,9 +327,10 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel": "k_safe_step", "bytes_per_env_step": bps, "bytes_per_launch": B * bps,
-                     "kernel_ms": round(kern_ms, 5),
+                     "kernel_ms": round(kern_ms, 5), "host_submit_ms": round(t_sub * 1e3, 4),
                      "timing": "achieved = bytes_per_launch / kernel_ms; kernel_ms = HIP events around the timed "
-                               "region / steps (includes the graph launch and the inter-kernel gaps)"},
+                               "region / steps (includes the graph launch and the inter-kernel gaps); host_submit_ms "
+                               "= host time spent in the graph replay calls"},
     }
     if extra:
         rec["extra"] = extra

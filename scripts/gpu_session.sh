@@ -2,7 +2,7 @@
 # One GPU-box session: each GPU step under its own time limit; a fault,
 # abort, segfault or time-out ends the session (no further GPU step).
 # Usage: bash scripts/gpu_session.sh TAG step [step ...]
-#   steps: smoke | pytest | bench | benchx
+#   steps: smoke | pytest | bench | driver (the driver's 20-step form) | benchx
 #          b_<w> | prof_<w> | pmc_<w> | sq_<w>    with workload <w> = cars | uni3 | uni5
 #          (bench.py without the CPU baseline;
 #           rocprofv3 kernel-trace stats; FETCH_SIZE and WRITE_SIZE passes;
@@ -46,6 +46,7 @@ for step in "$@"; do
     smoke)  run smoke 400 python __graft_entry__.py smoke ;;
     pytest) run pytest 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;
+    driver) run driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     benchx) run benchx 600 python bench.py --extra --no-cpu-baseline ;;
     b_*)    run "b_$wl" 300 python bench.py --no-cpu-baseline $(wl_args "$wl") ;;
     prof_*)
