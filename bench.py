@@ -526,24 +526,7 @@ def generic_qp_rows(layer, dev):
             G = torch.randn(B, m, n, device=dev, generator=gen)
             z0 = 0.3 * torch.randn(B, n, device=dev, generator=gen)
             h = (torch.einsum("bmn,bn->bm", G, z0) + 0.5 * torch.randn(B, m, device=dev, generator=gen).abs()).contiguous()
-            z = torch.empty(B, n, device=dev)
-            gz = torch.randn(B, n, device=dev, generator=gen)
-            gP, gq, gG, gh = torch.empty_like(P), torch.empty_like(q), torch.empty_like(G), torch.empty_like(h)
-            prm = ctypes.byref(layer._prm)
-
-            def fwd():
-                lib.rcbf_qp_solve(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(z),
-                                  None, None, None, _lib.stream_of(dev))
-
-            def bwd():
-                lib.rcbf_qp_backward(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(gz),
-                                     _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh), _lib.stream_of(dev))
-            by_in = 4 * (n * n + n + m * n + m)
-            fms, bms = _time_graph(fwd, 200, dev), _time_graph(bwd, 200, dev)
-            out[f"qp_n{n}_m{m}_B{B}"] = {
-                "fwd_us": round(fms * 1e3, 2), "bwd_us": round(bms * 1e3, 2),
-                "fwd_GBs": round(B * (by_in + 4 * n) / fms / 1e6, 1),
-                "bwd_GBs": round(B * (2 * by_in + 4 * n) / bms / 1e6, 1)}
+            out[f"qp_n{n}_m{m}_B{B}"] = _qp_pair_times(lib, layer._prm, P, q, G, h, gen, dev)
     # the layer's own rows (diagonal P, q = 0, slack/actuator structure): solve_qp as
     # get_safe_action calls it -- the closed-form path
     from rcbf_amd.diff_cbf_qp import CBFQPLayer
@@ -565,25 +548,42 @@ def generic_qp_rows(layer, dev):
         mu = torch.zeros(B, env.n_s, device=dev)
         sg = torch.full((B, env.n_s), 0.2, device=dev)
         P, q, G, h = (t.contiguous() for t in lay.get_cbf_qp_constraints(x, u, mu, sg))
-        n, m = G.shape[2], G.shape[1]
-        z = torch.empty(B, n, device=dev)
-        prm = ctypes.byref(lay._prm)
-
-        def fwd_l():
-            lib.rcbf_qp_solve(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(z),
-                              None, None, None, _lib.stream_of(dev))
-        gz = torch.randn(B, n, device=dev, generator=gen)
-        gP, gq, gG, gh = torch.empty_like(P), torch.empty_like(q), torch.empty_like(G), torch.empty_like(h)
-
-        def bwd_l():
-            lib.rcbf_qp_backward(prm, B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1, _lib.ptr(gz),
-                                 _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh), _lib.stream_of(dev))
-        fms, bms = _time_graph(fwd_l, 200, dev), _time_graph(bwd_l, 200, dev)
-        by_in = 4 * (n * n + n + m * n + m)
-        out[f"qp_layer_rows_{name}_B{B}"] = {"fwd_us": round(fms * 1e3, 2), "bwd_us": round(bms * 1e3, 2),
-                                             "fwd_GBs": round(B * (by_in + 4 * n) / fms / 1e6, 1),
-                                             "bwd_GBs": round(B * (2 * by_in + 4 * n) / bms / 1e6, 1)}
+        out[f"qp_layer_rows_{name}_B{B}"] = _qp_pair_times(lib, lay._prm, P, q, G, h, gen, dev)
     return out
+
+
+def _qp_pair_times(lib, prm_struct, P, q, G, h, gen, dev):
+    """Forward and backward launch times of one batch of QPs, row-normalised,
+    as the autograd surface runs them: rcbf_qp_solve_saved (z and the saved
+    fp64 solution) then rcbf_qp_backward_saved from it; plus the backward
+    that re-solves (rcbf_qp_backward).  Algorithmic bytes per QP: fwd P, q,
+    G, h in + z out (+ the saved z64), bwd the same in + z64 + grad_z in +
+    grad_P, grad_q, grad_G, grad_h out."""
+    import ctypes
+    from rcbf_amd import _lib
+    B, m, n = G.shape
+    z = torch.empty(B, n, device=dev)
+    z64 = torch.empty(B, n, dtype=torch.float64, device=dev)
+    gz = torch.randn(B, n, device=dev, generator=gen)
+    gP, gq, gG, gh = torch.empty_like(P), torch.empty_like(q), torch.empty_like(G), torch.empty_like(h)
+    prm = ctypes.byref(prm_struct)
+    ins = [_lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h), 1]
+    grads = [_lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh)]
+
+    def fwd():
+        lib.rcbf_qp_solve_saved(prm, B, n, m, *ins, _lib.ptr(z), _lib.ptr(z64), None, None, _lib.stream_of(dev))
+
+    def bwd():
+        lib.rcbf_qp_backward_saved(prm, B, n, m, *ins, _lib.ptr(z64), _lib.ptr(gz), *grads, _lib.stream_of(dev))
+
+    def bwd_resolve():
+        lib.rcbf_qp_backward(prm, B, n, m, *ins, _lib.ptr(gz), *grads, _lib.stream_of(dev))
+    fms = _time_graph(fwd, 200, dev)
+    bms, rms = _time_graph(bwd, 200, dev), _time_graph(bwd_resolve, 200, dev)
+    by_in = 4 * (n * n + n + m * n + m)
+    return {"fwd_us": round(fms * 1e3, 2), "bwd_us": round(bms * 1e3, 2), "bwd_resolve_us": round(rms * 1e3, 2),
+            "fwd_GBs": round(B * (by_in + 12 * n) / fms / 1e6, 1),
+            "bwd_GBs": round(B * (2 * by_in + 12 * n) / bms / 1e6, 1)}
 
 
 def _time_graph(fn, reps, dev):

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 5
+#define RCBF_ABI_VERSION 6
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -128,6 +128,25 @@ int rcbf_qp_backward(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, co
                      const float* q, const float* G, const float* h, int32_t normalize,
                      const float* grad_z, float* grad_P, float* grad_q, float* grad_G,
                      float* grad_h, hipStream_t stream);
+
+/* The forward/backward pair with the forward's solution saved, as qpth's
+ * QPFunction keeps zhats / lams for its backward (diff_cbf_qp.py:139; the
+ * autograd surface of solve_qp / cbf_layer uses this pair).
+ * rcbf_qp_solve_saved: rcbf_qp_solve that also writes the fp64 solution
+ * z64_saved (B,n).  rcbf_qp_backward_saved: rcbf_qp_backward that starts from
+ * z64_saved instead of re-solving: for a diagonal P and q = 0 the tight rows,
+ * multipliers and adjoint come from one factorisation on them; a QP whose
+ * KKT certificate fails there (or a full P / nonzero q) re-solves exactly,
+ * as rcbf_qp_backward does.  z64_saved must come from rcbf_qp_solve_saved on
+ * the same inputs. */
+int rcbf_qp_solve_saved(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P,
+                        const float* q, const float* G, const float* h, int32_t normalize,
+                        float* z_out, double* z64_saved, int32_t* status_out, int32_t* fail_flag,
+                        hipStream_t stream);
+int rcbf_qp_backward_saved(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P,
+                           const float* q, const float* G, const float* h, int32_t normalize,
+                           const double* z64_saved, const float* grad_z, float* grad_P,
+                           float* grad_q, float* grad_G, float* grad_h, hipStream_t stream);
 
 /* CBFQPLayer.get_safe_action (diff_cbf_qp.py:44-79), fused in one kernel:
  * build -> normalise -> fp64 QP -> .float() -> clamp(u_rl + u_qp, u_min, u_max).
@@ -273,9 +292,14 @@ int rcbf_env_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int
  * batch that lives on the device but talks to the host: the action is READ
  * from host memory and obs64 / reward / cost / done / goal_met are WRITTEN
  * to host memory by the kernel itself (zero copy, both buffers from
- * rcbf_host_alloc), then the call waits for the stream.  One host call, no
- * copy launches.  packed_host (8 B (n_o + 2) + 2 B bytes) holds
- *   obs64 (B, n_o) f64 | reward (B,) f64 | cost (B,) f64 | done (B,) u8 | goal_met (B,) u8.
+ * rcbf_host_alloc).  One host call, no copy launches.  For B <= 256 the
+ * kernel then stores a sequence number into a completion word in
+ * packed_host, after a system-scope fence, and the call returns once the
+ * word holds it (polling; the stream is asked every 4096 polls, so a failed
+ * kernel returns its error); for larger B the call waits for the stream.
+ * packed_host (W + 4 bytes, W = (B (8 (n_o + 2) + 2) + 7) & ~7) holds
+ *   obs64 (B, n_o) f64 | reward (B,) f64 | cost (B,) f64 | done (B,) u8 | goal_met (B,) u8
+ *   | pad to 8 B | completion word u32 at byte offset W.
  * action_host (B, n_u) f32 (action_f64 = 0) or f64 (action_f64 = 1).
  * Same arithmetic as rcbf_env_step. */
 int rcbf_env_step_sync(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step,

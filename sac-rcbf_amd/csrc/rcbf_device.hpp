@@ -1645,8 +1645,9 @@ __device__ __forceinline__ void uni_state32_from_cs(const double* xs, double c, 
     const double dc = (double)c32 - c, ds = (double)s32f - s;
     const double k = rint(xs[2] * (1.0 / k2PiHi));
     double t0 = fma(-k, k2PiLo, fma(-k, k2PiHi, xs[2]));  // the angle of (c, s), up to ~1e-16 k
-    const double den = fma(c, c, s * s);
-    double t = t0 + fma(c, ds, -s * dc) * rcp64_qp_nz(den);  // the angle of (c32, s32)
+    // the angle of (c32, s32): t0 + (c ds - s dc) / (c^2 + s^2), where c^2 + s^2 = 1 within a few ulps,
+    // so dividing the ~1e-8 correction by it would change t by ~1e-24 -- it is left out
+    double t = t0 + fma(c, ds, -s * dc);
     const double wrap = (s32f > 0.0f && t < 0.0) ? k2PiHi : ((s32f < 0.0f && t > 0.0) ? -k2PiHi : 0.0);
     t += wrap;
     t0 += wrap;
@@ -1924,8 +1925,10 @@ __device__ __forceinline__ void uni_env_step(const rcbf_params& prm, double* xs,
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+        // one v_mad_u64_u32 per 32 x 32 -> 64 product (hi and lo together)
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
         c[0] = n0;
         c[1] = lo1;

@@ -2,6 +2,8 @@
 // rcbf_env_reset, rcbf_env_step, rcbf_env_step_sync, rcbf_safe_step (the hot
 // path bench.py measures; kernel in rcbf_safe_step.hpp), rcbf_safe_step_seq,
 // rcbf_safe_rollout, host buffers, version/ABI queries.
+#include <atomic>
+
 #include "rcbf_safe_step.hpp"
 
 using namespace rcbf;
@@ -30,16 +32,14 @@ __global__ void __launch_bounds__(kBlock) k_env_reset(rcbf_params prm, int64_t B
 }
 
 template <int MODE, typename A>
-__global__ void __launch_bounds__(kBlock) k_env_step(rcbf_params prm, int64_t B, double* __restrict__ x,
-                                                     double* __restrict__ aux, int32_t* __restrict__ step,
-                                                     uint32_t* __restrict__ episode, const A* __restrict__ action,
-                                                     double* __restrict__ obs64, float* __restrict__ obs32,
-                                                     double* __restrict__ reward, double* __restrict__ cost,
-                                                     uint8_t* __restrict__ done, uint8_t* __restrict__ goal_met,
-                                                     int auto_reset, uint64_t seed, int64_t off) {
+__device__ __forceinline__ void env_step_one(const rcbf_params& prm, int64_t B, int64_t i, double* __restrict__ x,
+                                             double* __restrict__ aux, int32_t* __restrict__ step,
+                                             uint32_t* __restrict__ episode, const A* __restrict__ action,
+                                             double* __restrict__ obs64, float* __restrict__ obs32,
+                                             double* __restrict__ reward, double* __restrict__ cost,
+                                             uint8_t* __restrict__ done, uint8_t* __restrict__ goal_met,
+                                             int auto_reset, uint64_t seed, int64_t off) {
     using D = Dims<MODE, 1>;
-    int64_t i = env_index();
-    if (i < 0 || i >= B) return;
     double xs[D::NS];
     load_state<MODE>(x, B, i, xs);
     double a = aux[i];
@@ -77,6 +77,45 @@ __global__ void __launch_bounds__(kBlock) k_env_step(rcbf_params prm, int64_t B,
         for (int k = 0; k < D::NO; ++k) obs64[i * D::NO + k] = o[k];
     }
     if (obs32) store_obs32<MODE>(obs32, i, xs);
+}
+
+template <int MODE, typename A>
+__global__ void __launch_bounds__(kBlock) k_env_step(rcbf_params prm, int64_t B, double* __restrict__ x,
+                                                     double* __restrict__ aux, int32_t* __restrict__ step,
+                                                     uint32_t* __restrict__ episode, const A* __restrict__ action,
+                                                     double* __restrict__ obs64, float* __restrict__ obs32,
+                                                     double* __restrict__ reward, double* __restrict__ cost,
+                                                     uint8_t* __restrict__ done, uint8_t* __restrict__ goal_met,
+                                                     int auto_reset, uint64_t seed, int64_t off) {
+    int64_t i = env_index();
+    if (i < 0 || i >= B) return;
+    env_step_one<MODE, A>(prm, B, i, x, aux, step, episode, action, obs64, obs32, reward, cost, done, goal_met,
+                          auto_reset, seed, off);
+}
+
+// The same step for one workgroup's worth of envs (B <= kBlock) whose results
+// go to host memory (rcbf_env_step_sync): once every lane's outputs are
+// written, one lane makes them visible system-wide and then stores `seq` to
+// the host completion word, which the calling thread polls -- the call
+// returns when the results are there, without waiting for the kernel-end
+// cache actions and the completion signal behind hipStreamSynchronize.
+template <int MODE, typename A>
+__global__ void __launch_bounds__(kBlock) k_env_step_host(rcbf_params prm, int64_t B, double* __restrict__ x,
+                                                          double* __restrict__ aux, int32_t* __restrict__ step,
+                                                          uint32_t* __restrict__ episode, const A* __restrict__ action,
+                                                          double* __restrict__ obs64, double* __restrict__ reward,
+                                                          double* __restrict__ cost, uint8_t* __restrict__ done,
+                                                          uint8_t* __restrict__ goal_met, int auto_reset, uint64_t seed,
+                                                          int64_t off, uint32_t* done_word, uint32_t seq) {
+    const int64_t i = threadIdx.x;  // one workgroup
+    if (i < B)
+        env_step_one<MODE, A>(prm, B, i, x, aux, step, episode, action, obs64, nullptr, reward, cost, done, goal_met,
+                              auto_reset, seed, off);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();  // every lane's host writes land before the word
+        __hip_atomic_store(done_word, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 template <int MODE, int K>
@@ -193,10 +232,48 @@ int rcbf_env_step_sync(const rcbf_params* prm, int64_t B, double* x, double* aux
     double* cost = reward + B;
     uint8_t* done = reinterpret_cast<uint8_t*>(cost + B);
     uint8_t* goal = done + B;
-    int rc = rcbf_env_step(prm, B, x, aux, step, episode, action_host, action_f64, obs64, nullptr, reward, cost, done,
-                           goal, auto_reset, seed, env_offset, stream);
-    if (rc) return rc;
-    return (int)hipStreamSynchronize(stream);
+    if (B > kBlock) {  // several workgroups: wait for the stream
+        int rc = rcbf_env_step(prm, B, x, aux, step, episode, action_host, action_f64, obs64, nullptr, reward, cost,
+                               done, goal, auto_reset, seed, env_offset, stream);
+        if (rc) return rc;
+        return (int)hipStreamSynchronize(stream);
+    }
+    if (!x || !aux || !step || !action_host) return RCBF_E_NULL;
+    if (((uintptr_t)x) & 15) return RCBF_E_BAD_SHAPE;
+    // completion word: 4 bytes at the next 8-byte boundary after goal_met
+    const int64_t word_off = (B * (8 * (no + 2) + 2) + 7) & ~int64_t(7);
+    volatile uint32_t* word = reinterpret_cast<volatile uint32_t*>(reinterpret_cast<char*>(packed_host) + word_off);
+    static std::atomic<uint32_t> counter{0};
+    uint32_t seq = counter.fetch_add(1, std::memory_order_relaxed) + 1;
+    if (seq == 0 || seq == *word) seq = counter.fetch_add(1, std::memory_order_relaxed) + 1;
+#define RCBF_ENV_H(MODE, A)                                                                                         \
+    hipLaunchKernelGGL((k_env_step_host<MODE, A>), dim3(1), dim3(kBlock), 0, stream, *prm, B, x, aux, step, episode, \
+                       (const A*)action_host, obs64, reward, cost, done, goal, auto_reset, seed, env_offset,          \
+                       (uint32_t*)word, seq)
+    if (prm->mode == RCBF_MODE_SIMULATED_CARS) {
+        if (action_f64)
+            RCBF_ENV_H(RCBF_MODE_SIMULATED_CARS, double);
+        else
+            RCBF_ENV_H(RCBF_MODE_SIMULATED_CARS, float);
+    } else {
+        if (action_f64)
+            RCBF_ENV_H(RCBF_MODE_UNICYCLE, double);
+        else
+            RCBF_ENV_H(RCBF_MODE_UNICYCLE, float);
+    }
+#undef RCBF_ENV_H
+    if (int rc = launch_status()) return rc;
+    // poll the word; every 4096 polls ask the stream, so a kernel that fails
+    // (and never writes the word) returns its error instead of spinning
+    for (uint32_t n = 1;; ++n) {
+        if (*word == seq) return 0;
+        __builtin_ia32_pause();
+        if ((n & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess) return *word == seq ? 0 : (int)hipErrorUnknown;
+            if (q != hipErrorNotReady) return (int)q;
+        }
+    }
 }
 
 int rcbf_host_alloc(int64_t bytes, void** ptr) {

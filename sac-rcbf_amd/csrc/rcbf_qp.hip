@@ -384,11 +384,12 @@ __device__ __forceinline__ bool structured_kkt_adjoint(const StagedQP<N, MP, T>&
     int nact = 0;
     uint32_t amask = 0;
     bool ok = true;
+    T GAt[N][N];  // the tight rows, gathered in the rows' own type (one select per entry)
 #pragma unroll
     for (int sl = 0; sl < N; ++sl) {
         aidx[sl] = -1;
 #pragma unroll
-        for (int k = 0; k < N; ++k) GA[sl][k] = 0.0;
+        for (int k = 0; k < N; ++k) GAt[sl][k] = T(0);
     }
 #pragma unroll
     for (int r = 0; r < MP; ++r) {
@@ -402,12 +403,16 @@ __device__ __forceinline__ bool structured_kkt_adjoint(const StagedQP<N, MP, T>&
         for (int sl = 0; sl < N && sl <= r; ++sl) {  // row r can only land in slots 0..r
             const bool here = a && (sl == nact);
 #pragma unroll
-            for (int k = 0; k < N; ++k) GA[sl][k] = here ? (double)Q.G[r][k] : GA[sl][k];
+            for (int k = 0; k < N; ++k) GAt[sl][k] = here ? Q.G[r][k] : GAt[sl][k];
             aidx[sl] = here ? r : aidx[sl];
         }
         amask |= a ? (1u << r) : 0u;
         nact += a ? 1 : 0;
     }
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl)
+#pragma unroll
+        for (int k = 0; k < N; ++k) GA[sl][k] = (double)GAt[sl][k];
     double S[N][N], w1[N], w2[N], lam[N], Pg[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) Pg[k] = ip[k] * g[k];
@@ -466,7 +471,8 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_solve(rcbf_params prm, int64_t 
                                                        const T* __restrict__ q, const T* __restrict__ G,
                                                        const T* __restrict__ h, int normalize,
                                                        T* __restrict__ z_out, double* __restrict__ lam_out,
-                                                       int32_t* __restrict__ status_out, int32_t* fail_flag) {
+                                                       int32_t* __restrict__ status_out, int32_t* fail_flag,
+                                                       double* __restrict__ z64_out) {
     extern __shared__ __align__(16) unsigned char qp_smem[];
     T* sG = reinterpret_cast<T*>(qp_smem);
     T* sh = sG + kQPBlock * odd_stride(m * N);
@@ -516,6 +522,10 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_solve(rcbf_params prm, int64_t 
     }
 #pragma unroll
     for (int k = 0; k < N; ++k) z_out[i * N + k] = (T)res.z[k];
+    if (z64_out) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) z64_out[i * N + k] = res.z[k];
+    }
     if (lam_out) {
 #pragma unroll
         for (int r = 0; r < MP; ++r)
@@ -606,7 +616,7 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_bwd(rcbf_params prm, int64_t B,
                                                      const float* __restrict__ h, int normalize,
                                                      const float* __restrict__ grad_z, float* __restrict__ gP,
                                                      float* __restrict__ gq, float* __restrict__ gG,
-                                                     float* __restrict__ gh) {
+                                                     float* __restrict__ gh, const double* __restrict__ z64_in) {
     extern __shared__ __align__(16) unsigned char qp_smem[];
     float* sG = reinterpret_cast<float*>(qp_smem);
     float* sh = sG + kQPBlock * odd_stride(m * N);
@@ -656,17 +666,28 @@ __global__ void __launch_bounds__(kQPBlock) k_qp_bwd(rcbf_params prm, int64_t B,
 #pragma unroll
         for (int k = 0; k < N; ++k) pd[k] = active ? Q.P[k][k] : 1.0;
         pmat_set_diag_rt<N>(pm, pd);
-        // the layer's own rows: closed-form optimum, multipliers from stationarity (wave-uniform)
-        bool fast = false;
-        if (__ballot(active && !layer_structured<N, MP, float>(Q, m)) == 0) {
-            bool ok = true;
+        // The multipliers and the adjoint from ONE factorisation on the tight
+        // rows of the optimum (structured_kkt_adjoint, diagonal P, q = 0),
+        // where the optimum is the forward's saved fp64 solution (z64_in, what
+        // qpth's QPFunction keeps for its backward) or, on the layer's own
+        // rows, the closed-form one; a lane whose certificate fails re-solves
+        // with Goldfarb-Idnani.
+        bool need_gi = active;
+        if (z64_in) {
+            if (active && Q.qzero) {
+#pragma unroll
+                for (int k = 0; k < N; ++k) res.z[k] = z64_in[i * N + k];
+                res.status = RCBF_QP_OK;
+                need_gi = !structured_kkt_adjoint<N, MP, float>(Q, m, g, res, dz, eta, aidx);
+            }
+        } else if (__ballot(active && !layer_structured<N, MP, float>(Q, m)) == 0) {
             if (active) {
                 structured_solve<N, MP, float>(Q, m, res.z, res.status);
-                ok = res.status == RCBF_QP_OK && structured_kkt_adjoint<N, MP, float>(Q, m, g, res, dz, eta, aidx);
+                need_gi = !(res.status == RCBF_QP_OK &&
+                            structured_kkt_adjoint<N, MP, float>(Q, m, g, res, dz, eta, aidx));
             }
-            fast = __ballot(!ok) == 0;
         }
-        if (active && !fast) {
+        if (need_gi) {
             gi_solve<N, MP, true, float>(pm, Q.q, Q.G, Q.h, 4 * (MP + N) + 8, res);
             qp_adjoint<N, MP, true>(pm, Q, g, res, dz, eta, aidx);
         }
@@ -769,7 +790,7 @@ inline void allow_lds(const void* kernel, size_t bytes) {
 template <typename T>
 int qp_solve_launch(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const T* P, const T* q, const T* G,
                     const T* h, int32_t normalize, T* z_out, double* lam_out, int32_t* status_out,
-                    int32_t* fail_flag, hipStream_t stream) {
+                    int32_t* fail_flag, hipStream_t stream, double* z64_out = nullptr) {
     if (!prm) return RCBF_E_NULL;
     if (prm->solver != RCBF_SOLVER_ACTIVE_SET && prm->solver != RCBF_SOLVER_PDIPM && prm->solver != RCBF_SOLVER_GI)
         return RCBF_E_BAD_MODE;
@@ -783,11 +804,11 @@ int qp_solve_launch(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, con
         if (prm->solver == RCBF_SOLVER_PDIPM) {                                                                   \
             allow_lds(reinterpret_cast<const void*>(&k_qp_solve<RCBF_SOLVER_PDIPM, NN, MP, T>), lds);             \
             hipLaunchKernelGGL((k_qp_solve<RCBF_SOLVER_PDIPM, NN, MP, T>), g, b, lds, stream, *prm, B, m, P, q,  \
-                               G, h, normalize, z_out, lam_out, status_out, fail_flag);                           \
+                               G, h, normalize, z_out, lam_out, status_out, fail_flag, z64_out);                  \
         } else {                                                                                                  \
             allow_lds(reinterpret_cast<const void*>(&k_qp_solve<RCBF_SOLVER_GI, NN, MP, T>), lds);                \
             hipLaunchKernelGGL((k_qp_solve<RCBF_SOLVER_GI, NN, MP, T>), g, b, lds, stream, *prm, B, m, P, q, G,  \
-                               h, normalize, z_out, lam_out, status_out, fail_flag);                              \
+                               h, normalize, z_out, lam_out, status_out, fail_flag, z64_out);                     \
         }                                                                                                         \
     } while (0)
 #define RCBF_QP_M(NN)           \
@@ -801,7 +822,13 @@ int qp_solve_launch(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, con
         else                    \
             RCBF_QP_L(NN, 16);  \
     } while (0)
-    if (n == 1)
+    // the unicycle layer's rows at the reference's hazard counts 3 and 5 (m = 7, 9) get
+    // exact-size instantiations: no padding row in any per-row loop
+    if (sizeof(T) == 4 && n == 3 && m == 7)
+        RCBF_QP_L(3, 7);
+    else if (sizeof(T) == 4 && n == 3 && m == 9)
+        RCBF_QP_L(3, 9);
+    else if (n == 1)
         RCBF_QP_M(1);
     else if (n == 2)
         RCBF_QP_M(2);
@@ -829,9 +856,25 @@ int rcbf_qp_solve_f64(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, c
                                    stream);
 }
 
+int rcbf_qp_solve_saved(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P, const float* q,
+                        const float* G, const float* h, int32_t normalize, float* z_out, double* z64_saved,
+                        int32_t* status_out, int32_t* fail_flag, hipStream_t stream) {
+    if (!z64_saved) return RCBF_E_NULL;
+    return qp_solve_launch<float>(prm, B, n, m, P, q, G, h, normalize, z_out, nullptr, status_out, fail_flag, stream,
+                                  z64_saved);
+}
+
 int rcbf_qp_backward(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P, const float* q,
                      const float* G, const float* h, int32_t normalize, const float* grad_z, float* grad_P,
                      float* grad_q, float* grad_G, float* grad_h, hipStream_t stream) {
+    return rcbf_qp_backward_saved(prm, B, n, m, P, q, G, h, normalize, nullptr, grad_z, grad_P, grad_q, grad_G, grad_h,
+                                  stream);
+}
+
+int rcbf_qp_backward_saved(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, const float* P, const float* q,
+                           const float* G, const float* h, int32_t normalize, const double* z64_saved,
+                           const float* grad_z, float* grad_P, float* grad_q, float* grad_G, float* grad_h,
+                           hipStream_t stream) {
     if (!prm) return RCBF_E_NULL;
     if (B < 0 || n < 1 || n > 3 || m < 1 || m > 16) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
@@ -840,7 +883,7 @@ int rcbf_qp_backward(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, co
     const size_t lds = (size_t)qp_lds_words(n, m) * sizeof(float);
 #define RCBF_QPB_L(NN, MP)                                                                                       \
     hipLaunchKernelGGL((k_qp_bwd<NN, MP>), g, b, lds, stream, *prm, B, m, P, q, G, h, normalize, grad_z, grad_P, \
-                       grad_q, grad_G, grad_h)
+                       grad_q, grad_G, grad_h, z64_saved)
 #define RCBF_QPB_M(NN)           \
     do {                         \
         if (m <= 4)              \
@@ -852,7 +895,11 @@ int rcbf_qp_backward(const rcbf_params* prm, int64_t B, int32_t n, int32_t m, co
         else                     \
             RCBF_QPB_L(NN, 16);  \
     } while (0)
-    if (n == 1)
+    if (n == 3 && m == 7)
+        RCBF_QPB_L(3, 7);
+    else if (n == 3 && m == 9)
+        RCBF_QPB_L(3, 9);
+    else if (n == 1)
         RCBF_QPB_M(1);
     else if (n == 2)
         RCBF_QPB_M(2);

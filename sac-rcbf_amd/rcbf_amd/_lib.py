@@ -22,7 +22,7 @@ SOLVER_PDIPM = 1
 SOLVER_GI = 2
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NONFINITE = 0, 1, 2, 3
 MAX_HAZARDS = 8
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL"}
 
@@ -73,6 +73,8 @@ SIGNATURES = {
     "rcbf_qp_solve": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "rcbf_qp_solve_f64": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "rcbf_qp_backward": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P],
+    "rcbf_qp_solve_saved": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P],
+    "rcbf_qp_backward_saved": [_PRM, _I64, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_obs_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],

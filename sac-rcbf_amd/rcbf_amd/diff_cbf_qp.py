@@ -114,19 +114,21 @@ class _QP(torch.autograd.Function):
         lib = _lib.load()
         B, m, n = G.shape
         z = torch.empty(B, n, device=G.device)
+        z64 = torch.empty(B, n, dtype=torch.float64, device=G.device)  # kept for the backward, like qpth's zhats
         flag = _fail_flag(layer, G.device)
-        rc = lib.rcbf_qp_solve(ctypes.byref(layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G), _lib.ptr(h),
-                               int(normalize), _lib.ptr(z), None, None, _lib.ptr(flag), _lib.stream_of(G.device))
-        _lib.check(rc, "rcbf_qp_solve")
+        rc = lib.rcbf_qp_solve_saved(ctypes.byref(layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G),
+                                     _lib.ptr(h), int(normalize), _lib.ptr(z), _lib.ptr(z64), None, _lib.ptr(flag),
+                                     _lib.stream_of(G.device))
+        _lib.check(rc, "rcbf_qp_solve_saved")
         _raise_if_failed(flag)
         ctx.layer = layer
         ctx.normalize = normalize
-        ctx.save_for_backward(P, q, G, h)
+        ctx.save_for_backward(P, q, G, h, z64)
         return z
 
     @staticmethod
     def backward(ctx, grad_z):
-        P, q, G, h = ctx.saved_tensors
+        P, q, G, h, z64 = ctx.saved_tensors
         B, m, n = G.shape
         need = ctx.needs_input_grad
         gz = grad_z.to(torch.float32).contiguous()
@@ -134,10 +136,11 @@ class _QP(torch.autograd.Function):
         gq = torch.empty(B, n, device=G.device) if (need[3] and q is not None) else None
         gG = torch.empty_like(G) if need[4] else None
         gh = torch.empty_like(h) if need[5] else None
-        rc = _lib.load().rcbf_qp_backward(ctypes.byref(ctx.layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G),
-                                          _lib.ptr(h), int(ctx.normalize), _lib.ptr(gz), _lib.ptr(gP), _lib.ptr(gq),
-                                          _lib.ptr(gG), _lib.ptr(gh), _lib.stream_of(G.device))
-        _lib.check(rc, "rcbf_qp_backward")
+        rc = _lib.load().rcbf_qp_backward_saved(ctypes.byref(ctx.layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q),
+                                                _lib.ptr(G), _lib.ptr(h), int(ctx.normalize), _lib.ptr(z64),
+                                                _lib.ptr(gz), _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh),
+                                                _lib.stream_of(G.device))
+        _lib.check(rc, "rcbf_qp_backward_saved")
         return None, None, gP, gq, gG, gh
 
 

@@ -425,7 +425,8 @@ class _SingleEnv(_EnvBase):
         if io is not None:
             return io
         lib, b, n_o = _lib.load(), self._b, self.n_o
-        nbytes = 8 * (n_o + 2) + 2 + 16 + 16  # packed outputs | f32 action (2) | f64 action (2)
+        # packed outputs | pad | completion word (at 8 (n_o + 2) + 8) | f32 action (2) | f64 action (2)
+        nbytes = 8 * (n_o + 2) + 16 + 16 + 16
         p = ctypes.c_void_p()
         _lib.check(lib.rcbf_host_alloc(nbytes + 16, ctypes.byref(p)), "rcbf_host_alloc")
         base = (p.value + 15) & ~15

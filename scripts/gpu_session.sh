@@ -3,7 +3,7 @@
 # abort, segfault or time-out ends the session (no further GPU step).
 # Usage: bash scripts/gpu_session.sh TAG step [step ...]
 #   steps: smoke | pytest | bench | driver (the driver's 20-step form) | benchx
-#          b_<w> | prof_<w> | pmc_<w> | sq_<w>    with workload <w> = cars | uni3 | uni5
+#          b_<w> | prof_<w> | pmc_<w> | sq_<w>    with workload <w> = cars | uni3 | uni5 | carsT | uni5T
 #          (bench.py without the CPU baseline;
 #           rocprofv3 kernel-trace stats; FETCH_SIZE and WRITE_SIZE passes;
 #           SQ instruction counts -- each counter pass its own run)
@@ -28,17 +28,20 @@ wl_args() {  # bench.py arguments of a workload
     cars) echo "--env SimulatedCars" ;;
     uni3) echo "--env Unicycle --hazards 3" ;;
     uni5) echo "--env Unicycle --hazards 5" ;;
+    carsT) echo "--env SimulatedCars --prior tensor" ;;
+    uni5T) echo "--env Unicycle --hazards 5 --prior tensor" ;;
   esac
 }
 wl_kernel() {  # the fused kernel's name in rocprofv3 output
   case $1 in
-    cars) echo 'k_safe_step<0, 0, 1, false>' ;;
+    cars|carsT) echo 'k_safe_step<0, 0, 1, false>' ;;
     uni3) echo 'k_safe_step<0, 1, 3, false>' ;;
-    uni5) echo 'k_safe_step<0, 1, 5, false>' ;;
+    uni5|uni5T) echo 'k_safe_step<0, 1, 5, false>' ;;
   esac
 }
 wl_name() {
-  case $1 in cars) echo cars ;; uni3) echo unicycle3 ;; uni5) echo unicycle5 ;; esac
+  case $1 in cars) echo cars ;; uni3) echo unicycle3 ;; uni5) echo unicycle5 ;;
+    carsT) echo cars_tensorprior ;; uni5T) echo unicycle5_tensorprior ;; esac
 }
 for step in "$@"; do
   wl=${step#*_}

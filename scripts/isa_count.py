@@ -12,7 +12,7 @@ mangled = "k_safe_step" if False else name
 pat = "%d%s" % (len(name), name) + "IL" + "EL".join("i%d" % t for t in targs).replace("i", "i") + "E"
 sym = None
 for cand in re.findall(r"^(_Z\S+):", s, re.M):
-    if ("%d%s" % (len(name), name)) in cand and "".join("Li%dE" % t for t in targs) in cand:
+    if ("%d%s" % (len(name), name)) in cand and re.search("I" + "".join("L[ib]%dE" % t for t in targs) + "E", cand):
         sym = cand
         break
 if sym is None:

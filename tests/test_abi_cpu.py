@@ -66,6 +66,13 @@ def test_argument_validation_without_gpu():
                                 None) == 1003
     assert lib.rcbf_qp_backward(ctypes.byref(p), 0, 3, 7, None, None, None, None, 1, None, None, None, None, None,
                                 None) == 0
+    # the saved-solution pair: the forward requires the z64 buffer; the backward takes it nullable (re-solves)
+    assert lib.rcbf_qp_solve_saved(ctypes.byref(p), 4, 3, 7, None, None, None, None, 1, None, None, None, None,
+                                   None) == 1003
+    assert lib.rcbf_qp_backward_saved(ctypes.byref(p), 4, 4, 7, None, None, None, None, 1, None, None, None, None,
+                                      None, None, None) == 1002
+    assert lib.rcbf_qp_backward_saved(ctypes.byref(p), 4, 3, 7, None, None, None, None, 1, None, None, None, None,
+                                      None, None, None) == 1003
 
 
 def test_params_from_env_attributes():

@@ -216,3 +216,77 @@ def test_structured_backward_vs_oracle(golden, fixture, mode):
         assert ok.mean() > 0.9
         for k, got in (("P", gP), ("q", gq), ("G", gG), ("h", gh)):
             assert rel(got.cpu().numpy()[ok], want[k][ok]) <= 1e-5, (k, normalize)
+
+
+def _saved_pair(layer, P, q, G, h, w, normalize):
+    """rcbf_qp_solve_saved then rcbf_qp_backward_saved from its fp64 solution
+    (the autograd surface's pair); returns z and the four gradients."""
+    from rcbf_amd import _lib
+    lib = _lib.load()
+    B, m, n = G.shape
+    Pd, qd, Gd, hd, wd = dev(P), dev(q), dev(G), dev(h), dev(w)
+    z = torch.empty(B, n, device="cuda")
+    z64 = torch.empty(B, n, dtype=torch.float64, device="cuda")
+    gP, gq, gG, gh = torch.empty_like(Pd), torch.empty_like(qd), torch.empty_like(Gd), torch.empty_like(hd)
+    s = _lib.stream_of(Gd.device)
+    ins = [_lib.ptr(Pd), _lib.ptr(qd), _lib.ptr(Gd), _lib.ptr(hd), normalize]
+    assert lib.rcbf_qp_solve_saved(ctypes.byref(layer._prm), B, n, m, *ins, _lib.ptr(z), _lib.ptr(z64), None, None,
+                                   s) == 0
+    assert lib.rcbf_qp_backward_saved(ctypes.byref(layer._prm), B, n, m, *ins, _lib.ptr(z64), _lib.ptr(wd),
+                                      _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh), s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(z64.float(), z)
+    return z, {"P": gP, "q": gq, "G": gG, "h": gh}
+
+
+@pytest.mark.parametrize("diag", [False, True])
+@pytest.mark.parametrize("normalize", [0, 1])
+@pytest.mark.parametrize("n,m", [(2, 4), (3, 7), (3, 9), (2, 13)])
+def test_saved_pair_vs_oracle(n, m, normalize, diag):
+    """rcbf_qp_backward_saved from the forward's saved fp64 solution (one
+    factorisation on the tight rows for a diagonal P with q = 0, the exact
+    re-solve otherwise) equals the oracle's implicit-KKT derivative, like the
+    re-solving backward, on random QPs (dense P, q != 0; or diagonal P,
+    q = 0)."""
+    rng = np.random.default_rng(31 * n + m + 100 * normalize + 7 * diag)
+    B = 512
+    P, q, G, h = random_qps(rng, B, n, m)
+    if diag:
+        P = P * np.eye(n)[None]
+        q = np.zeros_like(q)
+    w = rng.normal(0, 1, (B, n)).astype(np.float32)
+    want = O.qp_backward(P, q, G, h, bool(normalize), w)
+    z, got = _saved_pair(_layer(), P, q, G, h, w, normalize)
+    ok = _non_degenerate(P, q, G, h, normalize)
+    assert ok.mean() > 0.9
+    assert rel(z.cpu().numpy()[ok], want["z"][ok]) <= 1e-6
+    for k in ("P", "q", "G", "h"):
+        assert rel(got[k].cpu().numpy()[ok], want[k][ok]) <= 1e-5, k
+
+
+@pytest.mark.parametrize("fixture", ["cars_layer", "unicycle3_layer", "unicycle5_layer"])
+def test_saved_pair_on_layer_rows_vs_oracle(golden, fixture):
+    """The saved pair on the layer's own rows (4096 reference-built rows, with
+    and without normalisation): the same gradients as the oracle and as the
+    re-solving rcbf_qp_backward."""
+    from rcbf_amd import _lib
+    d = golden(fixture)
+    G, h, P, q = (d["rand" + k].astype(np.float32) for k in ("_G", "_h", "_P", "_q"))
+    B, m, n = G.shape
+    w = np.random.default_rng(4).normal(0, 1, (B, n)).astype(np.float32)
+    layer = _layer()
+    lib = _lib.load()
+    for normalize in (0, 1):
+        want = O.qp_backward(P.astype(np.float64), q.astype(np.float64), G, h, bool(normalize), w)
+        _, got = _saved_pair(layer, P, q, G, h, w, normalize)
+        Pd, qd, Gd, hd, wd = dev(P), dev(q), dev(G), dev(h), dev(w)
+        ref = [torch.empty_like(t) for t in (Pd, qd, Gd, hd)]
+        assert lib.rcbf_qp_backward(ctypes.byref(layer._prm), B, n, m, _lib.ptr(Pd), _lib.ptr(qd), _lib.ptr(Gd),
+                                    _lib.ptr(hd), normalize, _lib.ptr(wd), *[_lib.ptr(t) for t in ref],
+                                    _lib.stream_of(Gd.device)) == 0
+        torch.cuda.synchronize()
+        ok = _non_degenerate(P.astype(np.float64), q.astype(np.float64), G, h, normalize)
+        assert ok.mean() > 0.9
+        for k, r in zip(("P", "q", "G", "h"), ref):
+            assert rel(got[k].cpu().numpy()[ok], want[k][ok]) <= 1e-5, (k, normalize)
+            assert rel(got[k].cpu().numpy()[ok], r.cpu().numpy()[ok]) <= 1e-6, (k, normalize)
