@@ -52,11 +52,23 @@ class DynamicsModel:
         if expand and t is not None:
             t = t.reshape(1)
         disturbance = (nxt - x - self.env.dt * self._f_plus_gu(x, u, t)) / self.env.dt
-        for i in range(x.shape[0]):
-            self.disturbance_history["state"][self.history_counter % self.max_history_count] = x[i]
-            self.disturbance_history["disturbance"][self.history_counter % self.max_history_count] = disturbance[i]
-            self.history_counter += 1
-            if self.history_counter % (self.max_history_count / 10) == 0:
+        # the reference's per-row loop (dynamics.py:263-290) as ring-buffer slices: rows are written in
+        # chunks that end where the reference refits the GP (history_counter % (max / 10) == 0), so every
+        # fit sees exactly the rows it does in the reference
+        cap, every = self.max_history_count, self.max_history_count / 10
+        i, n = 0, x.shape[0]
+        while i < n:
+            c = self.history_counter
+            nxt_fit = c + 1
+            if every == int(every) and every > 0:
+                nxt_fit = (c // int(every) + 1) * int(every)  # the next counter value that triggers a fit
+            take = min(n - i, nxt_fit - c) if every == int(every) and every > 0 else 1
+            slots = (c + np.arange(take)) % cap
+            self.disturbance_history["state"][slots] = x[i:i + take]
+            self.disturbance_history["disturbance"][slots] = disturbance[i:i + take]
+            self.history_counter += take
+            i += take
+            if self.history_counter % every == 0:
                 self.fit_gp_model()
 
     def fit_gp_model(self, training_iter=70):

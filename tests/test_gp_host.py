@@ -101,6 +101,35 @@ def test_append_transition_disturbance():
     assert np.array_equal(dm.disturbance_history["state"][:25], x)
 
 
+def test_append_transition_batches_wrap_the_ring():
+    """Batched appends (chunks of 1 .. 37 rows, 250 rows through a 100-row
+    ring) leave the ring, the counter and the fit points exactly as the
+    reference's row-by-row loop (dynamics.py:263-290) restated here."""
+    dm = _dyn("SimulatedCars")
+    snaps = []
+    dm.fit_gp_model = lambda *a, **k: snaps.append((dm.history_counter, dm.disturbance_history["state"].copy()))
+    rng = np.random.default_rng(8)
+    n = 250
+    x = rng.normal(30, 3, (n, 10)); u = rng.uniform(-1, 1, (n, 1)); t = rng.uniform(0, 6, n)
+    nx = x + rng.normal(0, 0.1, (n, 10))
+    ring_s, ring_d, cnt, want = np.zeros((100, 10)), np.zeros((100, 10)), 0, []
+    d = (nx - x - 0.02 * dm._f_plus_gu(x, u, t)) / 0.02
+    for i in range(n):  # the reference's loop
+        ring_s[cnt % 100], ring_d[cnt % 100] = x[i], d[i]
+        cnt += 1
+        if cnt % 10 == 0:
+            want.append((cnt, ring_s.copy()))
+    i = 0
+    for k in [1, 37, 5, 10, 3, 60, 19, 100, 15]:
+        dm.append_transition(x[i:i + k], u[i:i + k], nx[i:i + k], t[i:i + k])
+        i += k
+    assert i == n and dm.history_counter == n
+    assert [c for c, _ in snaps] == [c for c, _ in want]
+    assert all(np.array_equal(a, b) for (_, a), (_, b) in zip(snaps, want))
+    assert np.array_equal(dm.disturbance_history["state"], ring_s)
+    assert np.allclose(dm.disturbance_history["disturbance"], ring_d, rtol=0, atol=0)
+
+
 def test_get_dynamics_and_predict_next_obs(golden):
     """dynamics.py:107-188: get_dynamics' (f, g) rebuild the golden prior step
     x + dt (f + g u) (as the reference's predict_next_state uses them), and
