@@ -705,3 +705,65 @@ def test_torch_op_matches_python_function(mode, monkeypatch):
     with pytest.raises(Exception, match="QP Failed to solve"):
         layer.get_safe_action(dev(bad), dev(u), dev(mu), dev(sg))
     assert torch.equal(layer.get_safe_action(dev(s32), dev(u), dev(mu), dev(sg)), cpp[2])
+
+
+@pytest.mark.parametrize("mode", ["SimulatedCars", "Unicycle"])
+@pytest.mark.parametrize("B", [1, 7, 256, 300])
+def test_env_step_sync_matches_device_step(mode, B):
+    """rcbf_env_step_sync (the gym env.step path, main.py:95): action read
+    from and results written to pinned host memory; for B <= 256 the call
+    returns on the kernel's completion word, above that on the stream.  Its
+    packed obs64 / reward / cost / done / goal equal rcbf_env_step on device
+    buffers from the same state, and the completion word holds the call's
+    sequence number afterwards (so the outputs were complete when it returned)."""
+    import ctypes
+    from rcbf_amd import _lib
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+    lib = _lib.load()
+    mk = BatchedSimulatedCarsEnv if mode == "SimulatedCars" else BatchedUnicycleEnv
+    a_env, b_env = mk(B, seed=5), mk(B, seed=5)
+    rng = np.random.default_rng(B)
+    if mode == "SimulatedCars":
+        st = rng.integers(250, 300, B).astype(np.int32)
+        st[0] = 299  # env 0's episode ends (auto-reset on)
+        a_env.reset(noise=rng.normal(0, 0.5, B)); a_env.step_count.copy_(torch.as_tensor(st, device="cuda"))
+    else:
+        x0 = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        st = rng.integers(990, 1000, B).astype(np.int32)
+        st[0] = 999  # env 0's episode ends (auto-reset on)
+        a_env.load_state(x0, np.linalg.norm(x0[:, :2] - 2.5, axis=1), st)
+    b_env.load_state(a_env.state_numpy(), a_env.aux.cpu().numpy(), a_env.step_count.cpu().numpy().astype(np.int32))
+    b_env.episode.copy_(a_env.episode)
+    n_o, n_u = a_env.n_o, a_env.n_u
+    act = rng.uniform(-1, 1, (B, n_u)).astype(np.float32)
+    W = (B * (8 * (n_o + 2) + 2) + 7) & ~7
+    pk, ah = ctypes.c_void_p(), ctypes.c_void_p()
+    assert lib.rcbf_host_alloc(W + 8, ctypes.byref(pk)) == 0 and lib.rcbf_host_alloc(4 * B * n_u, ctypes.byref(ah)) == 0
+    try:
+        ctypes.memmove(ah.value, act.ctypes.data, act.nbytes)
+        word = ctypes.c_uint32.from_address(pk.value + W)
+        word.value = 0
+        rc = lib.rcbf_env_step_sync(ctypes.byref(a_env._prm_env), B, _lib.ptr(a_env.x), _lib.ptr(a_env.aux),
+                                    _lib.ptr(a_env.step_count), _lib.ptr(a_env.episode), ah, 0, pk, 1,
+                                    a_env._rng_seed(), a_env.env_offset, _lib.stream_of(torch.device("cuda")))
+        assert rc == 0
+        raw = (ctypes.c_char * W).from_address(pk.value).raw
+        seq = word.value
+        obs = np.frombuffer(raw, np.float64, B * n_o).reshape(B, n_o)
+        rew = np.frombuffer(raw, np.float64, B, 8 * B * n_o)
+        cost = np.frombuffer(raw, np.float64, B, 8 * B * (n_o + 1))
+        done = np.frombuffer(raw, np.uint8, B, 8 * B * (n_o + 2))
+        goal = np.frombuffer(raw, np.uint8, B, 8 * B * (n_o + 2) + B)
+    finally:
+        torch.cuda.synchronize()
+        lib.rcbf_host_free(pk)
+        lib.rcbf_host_free(ah)
+    _, r2, d2, info = b_env.step(dev(act), auto_reset=True, obs64=True)
+    torch.cuda.synchronize()
+    assert B > 256 or seq != 0
+    assert np.array_equal(obs, info["obs64"].cpu().numpy())
+    assert np.array_equal(rew, r2.cpu().numpy()) and np.array_equal(cost, info["cost"].cpu().numpy())
+    assert np.array_equal(done.astype(bool), d2.cpu().numpy()) and np.array_equal(goal.astype(bool),
+                                                                                     info["goal_met"].cpu().numpy())
+    assert np.array_equal(a_env.state_numpy(), b_env.state_numpy())
+    assert done[0]
