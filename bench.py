@@ -274,6 +274,15 @@ def main():
 
     if not args.cpu_dry_run:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # untimed rehearsal of the timed sequence (sync, event, replays, event, sync): the first
+        # such sequence after set-up spends ~35-50 us instead of ~15 us of host time in the replay
+        # call (profiles/r02/bench_rehearsal_r02y.txt); part of the warm-up, not of the K timed steps
+        sync()
+        ev0.record()
+        for _ in range(reps):
+            graph.replay()
+        ev1.record()
+        sync()
     shard.barrier(world)
     sync()
     t0 = time.perf_counter()
