@@ -74,7 +74,8 @@ __device__ __forceinline__ void st_out2(float* p, float a, float b) {
 
 // Phase timestamps of the fused step for the study build only
 // (csrc/study/rcbf_stamps.hip, scripts/stamps.py): lane 0 of every wave
-// records s_memtime at phase boundaries into buf as uint64 [wave][16].  The
+// records s_memtime at phase boundaries into buf as uint64 [wave][16], and
+// s_memrealtime (one 100 MHz clock for the whole chip) at its start and end.  The
 // product kernels use Stamps<false>, whose mark() compiles to nothing.
 template <bool ON>
 struct Stamps {
@@ -87,6 +88,11 @@ struct Stamps {
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
             __builtin_amdgcn_sched_barrier(0);
             if ((threadIdx.x & 63) == 0 && buf) buf[((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + j] = t;
+            if (j == 0 || j == 7) {  // the chip-wide 100 MHz clock at wave start / end, slots 10 / 11
+                const unsigned long long rt = __builtin_amdgcn_s_memrealtime();
+                if ((threadIdx.x & 63) == 0 && buf)
+                    buf[((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 16 + (j == 0 ? 10 : 11)] = rt;
+            }
         }
     }
     __device__ __forceinline__ void count(int j, bool lane_flag) const {

@@ -1195,6 +1195,61 @@ __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2
         bu1 = t ? u1 : bu1;
         bf = t ? f : bf;
     };
+    // stage 2's 1-D problem on an edge: the fixed coordinate at v, the free one
+    // y in [lo, hi]; e_j = al_j y + be_j and phi(y) = pf y^2 + (p_fixed v^2 +
+    // p2 eps(y)^2), convex, whose minimiser is the clamp of the unconstrained
+    // one, certified like stage 1 (origin: every be_j <= 0; piece j: e_j(y_j) > 0
+    // is the max) -> (ey, ef); nd gates its kink candidates by ballot
+    auto edge_solve = [&](bool fix0, double v, double lo, double hi, bool nd, double& ey, double& ef) {
+        double al[KK], be[KK];
+        bool eneg = true;
+#pragma unroll
+        for (int j = 0; j < KK; ++j) {
+            al[j] = fix0 ? a1[j] : a0[j];
+            be[j] = fix0 ? fma(a0[j], v, b[j]) : fma(a1[j], v, b[j]);
+            eneg = eneg && (be[j] <= 0.0);
+        }
+        const double pf = fix0 ? p1 : p0;
+        const double cfix = (fix0 ? p0 : p1) * v * v;
+        auto emax = [&](double y) {
+            double e = 0.0;
+#pragma unroll
+            for (int j = 0; j < KK; ++j) e = fmax(e, fma(al[j], y, be[j]));
+            return e;
+        };
+        auto fval = [&](double y) {
+            const double e = emax(y);
+            return fma(pf * y, y, fma(p2 * e, e, cfix));
+        };
+        ey = fmin(fmax(0.0, lo), hi);
+        ef = fval(ey);
+        bool eopen = !eneg;
+#pragma unroll
+        for (int j = 0; j < KK; ++j) {
+            const double yr = -(p2 * al[j] * be[j]) * rcp64_qp_nz(fma(p2 * al[j], al[j], pf));
+            const double ej = fma(al[j], yr, be[j]);
+            const bool cert = ej > 0.0 && ej >= emax(yr);
+            const double y = fmin(fmax(yr, lo), hi);
+            const double f = fval(y);
+            const bool t = eopen && (cert || f < ef);
+            ey = t ? y : ey;
+            ef = t ? f : ef;
+            eopen = eopen && !cert;
+        }
+        if (KK > 1 && __ballot(nd && eopen) != 0) {
+#pragma unroll
+            for (int i = 0; i < KK; ++i)
+#pragma unroll
+                for (int j = i + 1; j < KK; ++j) {
+                    // den = 0: NaN, which the clamp turns into the feasible point lo
+                    const double y = fmin(fmax((be[j] - be[i]) * rcp64_qp_nz(al[i] - al[j]), lo), hi);
+                    const double f = fval(y);
+                    const bool t = eopen && f < ef;
+                    ey = t ? y : ey;
+                    ef = t ? f : ef;
+                }
+        }
+    };
     bu0 = 0.0;
     bu1 = 0.0;
     bool all_neg = true;
@@ -1259,66 +1314,22 @@ __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2
     // u1-edge (where u_f1 leaves [L1, U1]), each only in waves with such a lane
     const double v0 = fmin(fmax(bu0, L0), U0), v1 = fmin(fmax(bu1, L1), U1);
     bf = inbox ? bf : __builtin_huge_val();  // an out-of-box stage-1 point must not win
-    auto edge = [&](bool fix0, double v, double lo, double hi, bool nd) {
-        // free coordinate y in [lo, hi]; e_j = al_j y + be_j and
-        // phi(y) = pf y^2 + (p_fixed v^2 + p2 eps(y)^2): a 1-D convex problem
-        // whose minimiser is the clamp of the unconstrained one, certified like
-        // stage 1 (origin: every be_j <= 0; piece j: e_j(y_j) > 0 is the max)
-        double al[KK], be[KK];
-        bool eneg = true;
-#pragma unroll
-        for (int j = 0; j < KK; ++j) {
-            al[j] = fix0 ? a1[j] : a0[j];
-            be[j] = fix0 ? fma(a0[j], v, b[j]) : fma(a1[j], v, b[j]);
-            eneg = eneg && (be[j] <= 0.0);
-        }
-        const double pf = fix0 ? p1 : p0;
-        const double cfix = (fix0 ? p0 : p1) * v * v;
-        auto emax = [&](double y) {
-            double e = 0.0;
-#pragma unroll
-            for (int j = 0; j < KK; ++j) e = fmax(e, fma(al[j], y, be[j]));
-            return e;
-        };
-        auto fval = [&](double y) {
-            const double e = emax(y);
-            return fma(pf * y, y, fma(p2 * e, e, cfix));
-        };
-        double ey = fmin(fmax(0.0, lo), hi);
-        double ef = fval(ey);
-        bool eopen = !eneg;
-#pragma unroll
-        for (int j = 0; j < KK; ++j) {
-            const double yr = -(p2 * al[j] * be[j]) * rcp64_qp_nz(fma(p2 * al[j], al[j], pf));
-            const double ej = fma(al[j], yr, be[j]);
-            const bool cert = ej > 0.0 && ej >= emax(yr);
-            const double y = fmin(fmax(yr, lo), hi);
-            const double f = fval(y);
-            const bool t = eopen && (cert || f < ef);
-            ey = t ? y : ey;
-            ef = t ? f : ef;
-            eopen = eopen && !cert;
-        }
-        if (KK > 1 && __ballot(nd && eopen) != 0) {
-#pragma unroll
-            for (int i = 0; i < KK; ++i)
-#pragma unroll
-                for (int j = i + 1; j < KK; ++j) {
-                    // den = 0: NaN, which the clamp turns into the feasible point lo
-                    const double y = fmin(fmax((be[j] - be[i]) * rcp64_qp_nz(al[i] - al[j]), lo), hi);
-                    const double f = fval(y);
-                    const bool t = eopen && f < ef;
-                    ey = t ? y : ey;
-                    ef = t ? f : ef;
-                }
-        }
-        const bool t = nd && ef < bf;
-        bu0 = t ? (fix0 ? v : ey) : bu0;
-        bu1 = t ? (fix0 ? ey : v) : bu1;
+    if (__ballot(need0) != 0) {
+        double ey, ef;
+        edge_solve(true, v0, L1, U1, need0, ey, ef);
+        const bool t = need0 && ef < bf;
+        bu0 = t ? v0 : bu0;
+        bu1 = t ? ey : bu1;
         bf = t ? ef : bf;
-    };
-    if (__ballot(need0) != 0) edge(true, v0, L1, U1, need0);
-    if (__ballot(need1) != 0) edge(false, v1, L0, U0, need1);
+    }
+    if (__ballot(need1) != 0) {
+        double ey, ef;
+        edge_solve(false, v1, L0, U0, need1, ey, ef);
+        const bool t = need1 && ef < bf;
+        bu0 = t ? ey : bu0;
+        bu1 = t ? v1 : bu1;
+        bf = t ? ef : bf;
+    }
 }
 
 // Wave-uniform maximum of a small per-lane count (0..K).

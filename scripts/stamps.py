@@ -55,7 +55,7 @@ P = ctypes.c_void_p
 slib.rcbf_study_safe_step_stamps.argtypes = [ctypes.POINTER(_lib.RcbfParams), ctypes.c_int64] + [P] * 11 + [
     ctypes.c_int32, ctypes.c_uint64, P]
 names = ["load", "get_state", "rows+norm", "QP", "env step", "obs+stores issued", "stores drained"]
-res, spans, late = [], [], []
+res, real = [], []
 fbs = []
 graph = "--eager" not in sys.argv  # default: steady state inside a hipGraph replay, like bench.py
 
@@ -88,13 +88,13 @@ for rep in range(30):
     if rep >= 10:
         t = st.view(nw, 16)[:, :8].cpu().numpy().astype(np.int64)
         res.append(np.diff(t, axis=1))
-        tw = t[(t > 0).all(1)]  # waves that wrote every stamp
-        spans.append(tw[:, 7].max() - tw[:, 0].min())
-        late.append(np.percentile(tw[:, 0] - tw[:, 0].min(), [50, 100]))
+        rt = st.view(nw, 16)[:, 10:12].cpu().numpy().astype(np.int64)
+        rt = rt[(rt > 0).all(1)]
+        real.append((rt[:, 1].max() - rt[:, 0].min(), np.percentile(rt[:, 0] - rt[:, 0].min(), 50),
+                     rt[:, 0].max() - rt[:, 0].min(), np.percentile(rt[:, 1] - rt[:, 0], 50)))
         fb = st.view(nw, 16)[:, 9].cpu().numpy()
         fbs = fbs + [fb] if rep > 10 else [fb]
 d = np.concatenate(res)
-spans, late = np.array(spans), np.array(late)
 print(f"B={B} ({'hipGraph replay' if graph else 'eager'}): per-phase s_memtime ticks per wave (median / p90), {d.shape[0]} wave samples")
 for k, n in enumerate(names):
     print(f"  {n:20s} {np.median(d[:, k]):8.0f} {np.percentile(d[:, k], 90):8.0f}")
@@ -102,5 +102,7 @@ fbv = np.concatenate(fbs)
 print(f"  lanes whose action the filter changed: {fbv.sum() / (64 * fbv.size):.4f}")
 tot = d.sum(1)
 print(f"  {'total':20s} {np.median(tot):8.0f} {np.percentile(tot, 90):8.0f}   p99 {np.percentile(tot, 99):.0f}  max {tot.max()}")
-print(f"  per launch: first wave start -> last wave end {np.median(spans):.0f} ticks (median over launches); "
-      f"wave start offsets median {np.median(late[:, 0]):.0f}, last {np.median(late[:, 1]):.0f}")
+rl = np.array(real) * 0.01  # s_memrealtime ticks (100 MHz) -> us
+print(f"  chip clock (s_memrealtime, us, median over launches): first wave start -> last wave end {np.median(rl[:, 0]):.2f}; "
+      f"wave start offsets median {np.median(rl[:, 1]):.2f}, last {np.median(rl[:, 2]):.2f}; wave lifetime median "
+      f"{np.median(rl[:, 3]):.2f}")
