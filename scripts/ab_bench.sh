@@ -1,4 +1,7 @@
-# A/B of two library builds in one session (temporary study script)
+# A/B of two library builds in one GPU session: the product librcbf_hip.so ("new") against
+# sac-rcbf_amd/rcbf_amd/librcbf_hip_old.so ("old", e.g. one TU rebuilt from the previous source),
+# alternating, 3 rounds, bench.py without the CPU baseline; one line per run in gpurun_out/TAG/sum.txt.
+# Usage: bash scripts/ab_bench.sh TAG workload [workload ...]   (workload = cars | u3 | u5 | drv)
 cd "${GRAFT_REPO_ROOT:-.}"; O=gpurun_out/$1; shift; mkdir -p $O
 V=sac-rcbf_amd/rcbf_amd/librcbf_hip_old.so
 for r in 1 2 3; do for w in "$@"; do
