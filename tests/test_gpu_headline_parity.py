@@ -193,3 +193,52 @@ def test_safe_step_seq_equals_single_steps():
         b.safe_step(us[k % 7], lb, outputs=ob)
     assert torch.equal(a.state, b.state) and torch.equal(a.step_count, b.step_count)
     assert torch.equal(a.obs, b.obs) and all(torch.equal(oa[k], ob[k]) for k in oa)
+
+
+@pytest.mark.parametrize("mode,k,prior", [("SimulatedCars", 3, "prior"), ("SimulatedCars", 3, "tensor"),
+                                          ("Unicycle", 3, "prior"), ("Unicycle", 5, "tensor")])
+def test_graph_replay_equals_eager_steps(mode, k, prior):
+    """What bench.py times -- a hipGraph of S fused launches captured on a side
+    stream, u_RL cycled from a pool, replayed on the current stream -- equals
+    the same S x replays eager safe_step calls bit for bit (state, reset
+    counters, observations and every output), auto-resets and, for prior =
+    "tensor", per-env mean/sigma included.  B = 65536, the headline size."""
+    B, S, reps = 65536, 20, 3
+    a, la = _make(mode, B, k)
+    b, lb = _make(mode, B, k)
+    gen = torch.Generator(device=a.device)
+    gen.manual_seed(7)
+    bench.init_states(a, gen, mode)
+    b.load_state(a.state, a.aux, a.step_count)
+    b.episode.copy_(a.episode)
+    pool = [(torch.rand(B, a.n_u, device=a.device, generator=gen) * 2 - 1).contiguous() for _ in range(S)]
+    mean = sigma = None
+    if prior == "tensor":
+        mean = (0.01 * torch.randn(B, a.n_s, device=a.device, generator=gen)).contiguous()
+        sigma = (0.2 * torch.rand(B, a.n_s, device=a.device, generator=gen) + 0.05).contiguous()
+    oa, ob = a.make_outputs(), b.make_outputs()
+    # one eager step each first (bench.py warms up the same way); capturing
+    # then records the launches without running them
+    a.safe_step(pool[0], la, mean=mean, sigma=sigma, outputs=oa)
+    b.safe_step(pool[0], lb, mean=mean, sigma=sigma, outputs=ob)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for j in range(S):
+            a.safe_step(pool[j], la, mean=mean, sigma=sigma, outputs=oa)
+    torch.cuda.synchronize()
+    assert torch.equal(a.state, b.state), "capture must not execute the steps"
+    for _ in range(reps):
+        g.replay()
+        for j in range(S):
+            b.safe_step(pool[j], lb, mean=mean, sigma=sigma, outputs=ob)
+    torch.cuda.synchronize()
+    assert torch.equal(a.state, b.state) and torch.equal(a.aux, b.aux)
+    assert torch.equal(a.step_count, b.step_count) and torch.equal(a.episode, b.episode)
+    assert torch.equal(a.obs, b.obs)
+    for key in oa:
+        if oa[key] is not None:
+            assert torch.equal(oa[key], ob[key]), key
+    assert int(a.episode.max().item()) >= 1 or mode == "Unicycle"  # cars episodes roll over inside 60 steps
+    a.check_failures()
+    b.check_failures()
