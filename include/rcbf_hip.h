@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 6
+#define RCBF_ABI_VERSION 7
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -241,6 +241,16 @@ int rcbf_model_step(const rcbf_params* prm, int64_t B, const double* obs, const 
                     const double* t, const float* mean, const float* std, const double* z,
                     uint64_t seed, uint64_t counter, double* next_obs, double* reward,
                     double* mask, double* next_t, hipStream_t stream);
+
+/* DynamicsModel.predict_next_state (rcbf_sac/dynamics.py:60-105) on device
+ * rows, fp64: next_x = x + dt (f(x) + g(x) u) (+ dt * mean when use_gps),
+ * std_out = dt * std (zeros when !use_gps), next_t = t + dt [nullable].
+ * x (B,n_s) f64, act (B,n_u) f64, t (B,) f64 [nullable for the unicycle];
+ * mean/std (B,n_s) f32, the GP posterior [nullable: the zero-mean MAX_STD
+ * prior, dynamics.py:381-384]. */
+int rcbf_predict_next_state(const rcbf_params* prm, int64_t B, const double* x, const double* act,
+                            const double* t, const float* mean, const float* std, int32_t use_gps,
+                            double* next_x, double* std_out, double* next_t, hipStream_t stream);
 
 /* ReplayMemory.batch_push (replay_memory.py:23-29) as one launch: n records
  * of W f64 (state, action, reward, next_state, mask, t, next_t packed) into

@@ -154,6 +154,49 @@ __global__ void __launch_bounds__(kBlock) k_model_step(rcbf_params prm, int64_t 
     if (next_t) next_t[i] = tn;
 }
 
+// DynamicsModel.predict_next_state (dynamics.py:60-105) on device rows:
+// next = x + dt (f(x) + g(x) u) [+ dt * mean when use_gps], std_out = dt * std
+// (zeros without use_gps), next_t = t + dt.  The disturbance (mean, std) is
+// the fitted GP's posterior (f32, rcbf_gp_predict) or, when null, the
+// zero-mean MAX_STD prior (dynamics.py:381-384).  fp64 rows, contraction off:
+// the same roundings as the reference's numpy.
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) k_predict_next_state(int64_t B, const double* __restrict__ x,
+                                                               const double* __restrict__ act,
+                                                               const double* __restrict__ t,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ stdv, int use_gps,
+                                                               double* __restrict__ next_x,
+                                                               double* __restrict__ std_out,
+                                                               double* __restrict__ next_t) {
+#pragma clang fp contract(off)
+    using D = Dims<MODE, 1>;
+    constexpr int NS = D::NS, NU = D::NU;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    const double dt = 0.02;
+    double xs[NS], u[NU], nx[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) xs[k] = x[i * NS + k];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) u[c] = act[i * NU + c];
+    const double ti = t ? t[i] : 0.0;
+    model_prior_next<MODE>(xs, u, ti, nx);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        double sd = 0.0;
+        if (use_gps) {
+            const double m = mean ? (double)mean[i * NS + k] : 0.0;
+            const double prior = (MODE == RCBF_MODE_UNICYCLE || (k & 1)) ? 0.2 : 0.0;  // MAX_STD
+            sd = stdv ? (double)stdv[i * NS + k] : prior;
+            nx[k] = nx[k] + dt * m;  // next_state_batch += dt * pred_mean
+        }
+        next_x[i * NS + k] = nx[k];
+        std_out[i * NS + k] = dt * sd;
+    }
+    if (next_t) next_t[i] = ti + dt;
+}
+
 // Replay ring (rcbf_sac/replay_memory.py:12-32): records are rows of W f64.
 __global__ void __launch_bounds__(256) k_ring_scatter(double* __restrict__ ring, int64_t cap, int64_t W, int64_t pos,
                                                       const double* __restrict__ src, int64_t n) {
@@ -190,6 +233,25 @@ int rcbf_model_step(const rcbf_params* prm, int64_t B, const double* obs, const 
     else
         hipLaunchKernelGGL((k_model_step<RCBF_MODE_UNICYCLE>), g, b, 0, stream, *prm, B, obs, act, t, mean, stdv, z,
                            seed, counter, next_obs, reward, mask, next_t);
+    return launch_status();
+}
+
+int rcbf_predict_next_state(const rcbf_params* prm, int64_t B, const double* x, const double* act, const double* t,
+                            const float* mean, const float* stdv, int32_t use_gps, double* next_x, double* std_out,
+                            double* next_t, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !act || !next_x || !std_out) return RCBF_E_NULL;
+    if (prm->mode == RCBF_MODE_SIMULATED_CARS && !t) return RCBF_E_NULL;  // cars dynamics need t
+    if (next_t && !t) return RCBF_E_NULL;
+    dim3 g(grid_for(B)), b(kBlock);
+    if (prm->mode == RCBF_MODE_SIMULATED_CARS)
+        hipLaunchKernelGGL((k_predict_next_state<RCBF_MODE_SIMULATED_CARS>), g, b, 0, stream, B, x, act, t, mean,
+                           stdv, (int)use_gps, next_x, std_out, next_t);
+    else
+        hipLaunchKernelGGL((k_predict_next_state<RCBF_MODE_UNICYCLE>), g, b, 0, stream, B, x, act, t, mean, stdv,
+                           (int)use_gps, next_x, std_out, next_t);
     return launch_status();
 }
 

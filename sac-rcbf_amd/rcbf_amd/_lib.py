@@ -22,7 +22,7 @@ SOLVER_PDIPM = 1
 SOLVER_GI = 2
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NONFINITE = 0, 1, 2, 3
 MAX_HAZARDS = 8
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL"}
 
@@ -79,6 +79,7 @@ SIGNATURES = {
     "rcbf_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_obs_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_gp_workspace_floats": [_GPM, _I64],
+    "rcbf_predict_next_state": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P],
     "rcbf_model_step": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _U64, _U64, _P, _P, _P, _P, _P],
     "rcbf_ring_scatter_f64": [_P, _I64, _I64, _I64, _P, _I64, _P],
     "rcbf_gather_rows_f64": [_P, _P, _I64, _P, _I64, _P],

@@ -3,7 +3,8 @@
 DYNAMICS_MODE / MAX_STD (dynamics.py:22-24), get_state / get_obs
 (:190-261), predict_disturbance (:342-390) with the zero-mean MAX_STD prior
 or, once fitted, the GP posterior on the device (rcbf_amd.gp, the
-rcbf_gp_predict kernel), predict_next_state (:60-105) and the disturbance
+rcbf_gp_predict kernel), predict_next_state (:60-105; device tensors through
+the rcbf_predict_next_state kernel) and the disturbance
 history + GP fit (append_transition / fit_gp_model, :263-340).
 
 Inside the fused step (rcbf_safe_step) get_state and the prior run in-kernel;
@@ -150,6 +151,16 @@ class DynamicsModel:
         return s[0] if expand else s
 
     def get_obs(self, state_batch):
+        if torch.is_tensor(state_batch):  # device rows stay on the device (fp64 like the numpy path)
+            expand = state_batch.dim() == 1
+            s = state_batch.reshape(-1, self.n_s).to(torch.float64)
+            if self.env.dynamics_mode == "Unicycle":
+                o = torch.stack([s[:, 0], s[:, 1], torch.cos(s[:, 2]), torch.sin(s[:, 2])], dim=1)
+            else:
+                o = s.clone()
+                o[:, ::2] /= 100.0
+                o[:, 1::2] /= 30.0
+            return o[0] if expand else o
         s = np.atleast_2d(np.asarray(state_batch, np.float64))
         if self.env.dynamics_mode == "Unicycle":
             return np.stack([s[:, 0], s[:, 1], np.cos(s[:, 2]), np.sin(s[:, 2])], axis=1)
@@ -185,6 +196,8 @@ class DynamicsModel:
 
     # -- model prior step (dynamics.py:60-105, 125-188) ---------------------
     def predict_next_state(self, state_batch, u_batch, t_batch=None, use_gps=True):
+        if torch.is_tensor(state_batch) and state_batch.is_cuda:
+            return self._predict_next_state_device(state_batch, u_batch, t_batch, use_gps)
         x = np.asarray(state_batch, np.float64)
         expand = x.ndim == 1
         x = np.atleast_2d(x)
@@ -201,6 +214,41 @@ class DynamicsModel:
         if t_batch is not None:
             return nxt, dt * std, t_batch + dt
         return nxt, dt * std, t_batch
+
+    def _predict_next_state_device(self, state_batch, u_batch, t_batch, use_gps):
+        """predict_next_state on device tensors: one rcbf_predict_next_state
+        launch (fp64, the numpy path's operation order); the GP posterior, once
+        fitted, from the rcbf_gp_predict kernel.  Returns tensors in the
+        state's dtype (next_t in float64)."""
+        import ctypes
+        from . import _lib
+        from .params import make_params
+        dev = state_batch.device
+        expand = state_batch.dim() == 1
+        x = state_batch.reshape(-1, self.n_s).to(torch.float64).contiguous()
+        B = x.shape[0]
+        u = torch.as_tensor(u_batch, device=dev).to(torch.float64).reshape(B, self.n_u).contiguous()
+        t = None
+        if t_batch is not None:
+            t = torch.as_tensor(t_batch, device=dev).to(torch.float64).reshape(B).contiguous()
+        mean = std = None
+        if use_gps and self.disturb_estimators:
+            mean, std = self.disturb_estimators.predict(x.to(torch.float32))
+            mean = mean.to(device=dev, dtype=torch.float32).contiguous()
+            std = std.to(device=dev, dtype=torch.float32).contiguous()
+        nxt, sd = torch.empty_like(x), torch.empty_like(x)
+        nt = None if t is None else torch.empty_like(t)
+        prm = make_params(self.env, 1.0)
+        rc = _lib.load().rcbf_predict_next_state(ctypes.byref(prm), B, _lib.ptr(x), _lib.ptr(u), _lib.ptr(t),
+                                                 _lib.ptr(mean), _lib.ptr(std), int(bool(use_gps)), _lib.ptr(nxt),
+                                                 _lib.ptr(sd), _lib.ptr(nt), _lib.stream_of(dev))
+        _lib.check(rc, "rcbf_predict_next_state")
+        nxt, sd = nxt.to(state_batch.dtype), sd.to(state_batch.dtype)
+        if expand:
+            nxt, sd = nxt[0], sd[0]
+        if t_batch is not None:
+            return nxt, sd, nt.reshape(torch.as_tensor(t_batch).shape)
+        return nxt, sd, t_batch
 
     def predict_next_obs(self, state, u):
         """dynamics.py:107-123: the mean next observation."""

@@ -113,3 +113,65 @@ def test_generate_model_rollouts_end_to_end():
     assert np.max(np.abs(R - rb)) <= 1e-12 and np.array_equal(M, mb) and np.array_equal(NT, tb)
     zh = (NS - base)[:, 1::2] * 30.0 / (0.02 * 0.2)
     assert np.all(np.abs(zh) < 7) and np.array_equal(NS[:, ::2], base[:, ::2])
+
+
+@pytest.mark.parametrize("nm,mode", [("cars", "SimulatedCars"), ("uni", "Unicycle")])
+def test_predict_next_state_device_vs_reference(golden, nm, mode):
+    """DynamicsModel.predict_next_state on device tensors (the
+    rcbf_predict_next_state kernel) against the reference's own outputs
+    (tests/golden/dynamics.npz, use_gps=False: bit-exact), the MAX_STD prior
+    (use_gps=True before a fit: dt * MAX_STD, mean 0), a GP posterior's
+    (mean, std) entering as next + dt * mean, dt * std, and the 1-D form."""
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.envs import SimulatedCarsEnv, UnicycleEnv
+    d = golden("dynamics")
+    env = SimulatedCarsEnv() if mode == "SimulatedCars" else UnicycleEnv()
+    dm = DynamicsModel(env, types.SimpleNamespace(cuda=True, gp_model_size=2000))
+    dev = torch.device("cuda", 0)
+    x = torch.as_tensor(d[nm + "_state_np"], device=dev)
+    u = torch.as_tensor(d[nm + "_u"], device=dev)
+    t = torch.as_tensor(d[nm + "_t"], device=dev) if nm + "_t" in d else None
+    nx, sd, nt = dm.predict_next_state(x, u, t_batch=t, use_gps=False)
+    assert nx.is_cuda and np.array_equal(nx.cpu().numpy(), d[nm + "_next"])
+    assert not sd.cpu().numpy().any()
+    if t is not None:
+        assert np.array_equal(nt.cpu().numpy(), d[nm + "_t"] + 0.02)
+    # the prior: mean 0, std dt * MAX_STD (the numpy path of the same class agrees)
+    nx2, sd2, _ = dm.predict_next_state(x, u, t_batch=t, use_gps=True)
+    ref_nx, ref_sd, _ = dm.predict_next_state(d[nm + "_state_np"], d[nm + "_u"],
+                                              t_batch=d.get(nm + "_t"), use_gps=True)
+    assert np.array_equal(nx2.cpu().numpy(), ref_nx) and np.array_equal(sd2.cpu().numpy(), ref_sd)
+    _, s_prior = O.predict_disturbance_prior(mode, x.shape[0])
+    assert np.array_equal(sd2.cpu().numpy(), 0.02 * s_prior)
+    # a fitted GP's posterior (stand-in estimator returning fixed f32 mean / std)
+    rng = np.random.default_rng(11)
+    m32 = rng.normal(0, 0.05, x.shape).astype(np.float32)
+    s32 = rng.uniform(0.01, 0.3, x.shape).astype(np.float32)
+
+    class _GP:
+        def predict(self, xq):
+            return torch.as_tensor(m32, device=xq.device), torch.as_tensor(s32, device=xq.device)
+    dm.disturb_estimators = _GP()
+    nx3, sd3, _ = dm.predict_next_state(x, u, t_batch=t, use_gps=True)
+    assert np.array_equal(nx3.cpu().numpy(), d[nm + "_next"] + 0.02 * m32.astype(np.float64))
+    assert np.array_equal(sd3.cpu().numpy(), 0.02 * s32.astype(np.float64))
+    # 1-D state: squeezed outputs, like the reference's expand_dims handling
+    dm.disturb_estimators = None
+    n1, s1, t1 = dm.predict_next_state(x[3], u[3], t_batch=None if t is None else t[3], use_gps=False)
+    assert n1.shape == (x.shape[1],) and np.array_equal(n1.cpu().numpy(), d[nm + "_next"][3])
+
+
+def test_predict_next_obs_device(golden):
+    """predict_next_obs (dynamics.py:107-123) on device tensors stays on the
+    device and equals the numpy path (cars: bit-exact; unicycle: the device
+    cos/sin within 1e-15)."""
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.envs import UnicycleEnv
+    d = golden("dynamics")
+    dm = DynamicsModel(UnicycleEnv(), types.SimpleNamespace(cuda=True))
+    x = torch.as_tensor(d["uni_state_np"], device="cuda")
+    u = torch.as_tensor(d["uni_u"], device="cuda")
+    o = dm.predict_next_obs(x, u)
+    ref = dm.predict_next_obs(d["uni_state_np"], d["uni_u"])
+    assert o.is_cuda and o.shape == ref.shape
+    assert np.max(np.abs(o.cpu().numpy() - ref)) <= 1e-15
