@@ -2,7 +2,7 @@
 # One GPU-box session: each GPU step under its own time limit; a fault,
 # abort, segfault or time-out ends the session (no further GPU step).
 # Usage: bash scripts/gpu_session.sh TAG step [step ...]
-#   steps: smoke | pytest | bench | driver (the driver's 20-step form) | benchx
+#   steps: smoke | pytest | bench | driver (the driver's 20-step form) | profdrv (it, traced) | benchx
 #          b_<w> | prof_<w> | pmc_<w> | sq_<w>    with workload <w> = cars | uni3 | uni5 | carsT | uni5T
 #          (bench.py without the CPU baseline;
 #           rocprofv3 kernel-trace stats; FETCH_SIZE and WRITE_SIZE passes;
@@ -57,6 +57,11 @@ for step in "$@"; do
         python3 bench.py --no-cpu-baseline $(wl_args "$wl")
       [ -f "$OUT/prof_$wl/run_kernel_trace.csv" ] && python scripts/trace_summary.py "$OUT/prof_$wl/run_kernel_trace.csv" \
         "$(wl_kernel "$wl")" "$OUT/$(wl_name "$wl")_B65536_kernel_trace_summary.json" ;;
+    profdrv)  # the driver's own command under the tracer
+      run profdrv 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profdrv" -o run -- \
+        python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
+      [ -f "$OUT/profdrv/run_kernel_trace.csv" ] && python scripts/trace_summary.py "$OUT/profdrv/run_kernel_trace.csv" \
+        "$(wl_kernel cars)" "$OUT/cars_B65536_driver_form_kernel_trace_summary.json" ;;
     pmc_*)
       run "pmcf_$wl" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcf_$wl" -o run -- \
         python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 $(wl_args "$wl")
