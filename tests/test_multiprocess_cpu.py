@@ -107,10 +107,12 @@ def test_bench_gpus_flag_launches_ranks():
     assert rec["value"] > 0 and "dry run" in rec["data"]
 
 
-def test_bench_under_torchrun_launcher():
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_under_torchrun_launcher(n):
     """The driver's N > 1 launch form: python -m torch.distributed.run
-    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 bench.py --gpus 2
-    (ranks from the torchrun environment, no second spawn), CPU dry run."""
+    --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+    (ranks from the torchrun environment, no second spawn), CPU dry run; N = 8
+    rehearses the driver's full-node scaling run."""
     import json
     import subprocess
     import sys
@@ -118,12 +120,13 @@ def test_bench_under_torchrun_launcher():
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
-                        "--gpus", "2", "--cpu-dry-run", "--steps", "4", "--warmup", "1", "--batch", "512"],
+                        "--gpus", str(n), "--cpu-dry-run", "--steps", "4", "--warmup", "1", "--batch", "512"],
                        capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
-    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 1024
+    assert rec["n_gpus"] == n and rec["config"]["global_batch"] == n * 512
+    assert rec["config"]["parallelism"] == f"env-shard x{n} (no collective)"
