@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--launch", default="graph", choices=["graph", "seq"],
                     help="graph: hipGraph replays of --graph-steps fused steps; seq: the K launches issued from "
                          "one host call (rcbf_safe_step_seq)")
+    ap.add_argument("--host-cores", type=int, default=4,
+                    help="host cores per rank for the launch threads (0: no pinning)")
     return ap.parse_args()
 
 
@@ -240,6 +242,21 @@ class _DryRun:
         pass
 
 
+def pin_host_cores(local, n):
+    """Keep this rank's host threads (the replay calls and the HIP runtime's
+    own threads, created after this) on n cores of their own, rank r on the
+    r-th group of the allowed CPUs, before anything touches the GPU.  The
+    replay call then takes 14-16 us instead of 18-34 us of host time in the
+    driver's 20-step form (profiles/r02/host_pinning_study_r02ag.txt).
+    Returns the original mask (restored for the CPU baseline), or None when
+    pinning is off or there are too few CPUs."""
+    allowed = sorted(os.sched_getaffinity(0))
+    if n <= 0 or len(allowed) < n * (local + 1):
+        return None
+    os.sched_setaffinity(0, set(allowed[n * local:n * (local + 1)]))
+    return set(allowed)
+
+
 def main():
     args = parse()
     from rcbf_amd import shard
@@ -253,6 +270,7 @@ def main():
             raise SystemExit("--scaling strong needs --batch divisible by the GPU count")
         args.batch //= world
     B = args.batch
+    host_mask = None
     if args.cpu_dry_run:
         dev = torch.device("cpu")
         if world > 1:
@@ -264,6 +282,7 @@ def main():
     else:
         if local >= torch.cuda.device_count():
             raise SystemExit(f"rank {rank}: LOCAL_RANK {local}, but {torch.cuda.device_count()} HIP device(s) visible")
+        host_mask = pin_host_cores(local, args.host_cores)
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if world > 1:
@@ -331,7 +350,8 @@ def main():
                                f"batch {B} envs per GPU, {args.solver} fp64 QP, {launch}",
                    "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
                    "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)",
-                   "prior": args.prior, "qp_active_frac_at_start": round(active_frac, 4)},
+                   "prior": args.prior, "qp_active_frac_at_start": round(active_frac, 4),
+                   "host_cores_per_rank": args.host_cores if host_mask else None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
@@ -344,6 +364,8 @@ def main():
     if extra:
         rec["extra"] = extra
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.cpu_dry_run:
+        if host_mask:  # the CPU baseline gets every allowed core back
+            os.sched_setaffinity(0, host_mask)
         rec["cpu_baseline"] = cpu_baseline(args.env, args.hazards, args.cpu_seconds)
         rec["cpu_reference_mode"] = cpu_reference_mode(args.env, args.hazards, args.cpu_seconds / 3)
     if rank == 0:
