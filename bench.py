@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--launch", default="graph", choices=["graph", "seq"],
                     help="graph: hipGraph replays of --graph-steps fused steps; seq: the K launches issued from "
                          "one host call (rcbf_safe_step_seq)")
+    ap.add_argument("--cpu-baseline-only", action="store_true",
+                    help="(internal) print the CPU baselines as JSON and exit; never touches the GPU")
     ap.add_argument("--host-cores", type=int, default=4,
                     help="host cores per rank for the launch threads (0: no pinning)")
     return ap.parse_args()
@@ -112,11 +114,30 @@ def cpu_baseline(env_name, hazards, seconds):
             if el >= budget or n >= 100000:
                 return n * B / el, n, el
 
-    v1, n1, e1 = run(1, seconds * 0.3)
-    vN, nN, eN = run(threads_all, seconds * 0.7)
-    return {"value": round(vN, 1), "unit": "safe env steps/s", "cores": threads_all, "kind": "port",
-            "sample": f"C oracle fused step (oracle/rcbf_oracle.c, exact QP), {nN} steps x {B} envs in "
-                      f"{eN:.1f} s on {threads_all} threads; 1 thread: {v1:.4g} steps/s ({n1} steps)"}
+    v1, n1, e1 = run(1, seconds * 0.25)
+    run(threads_all, min(1.0, seconds * 0.05))  # untimed: the OpenMP pool's start-up (tens of ms per step at first)
+    samples = [run(threads_all, seconds * 0.25) for _ in range(3)]
+    rates = sorted(v for v, _, _ in samples)
+    nN, eN = sum(n for _, n, _ in samples), sum(e for _, _, e in samples)
+    return {"value": round(rates[1], 1), "unit": "safe env steps/s", "cores": threads_all, "kind": "port",
+            "sample": f"C oracle fused step (oracle/rcbf_oracle.c, exact QP, gcc -O3 -march=x86-64-v3), median of 3 "
+                      f"samples on {threads_all} threads ({rates[0]:.4g} / {rates[1]:.4g} / {rates[2]:.4g} steps/s; "
+                      f"{nN} steps x {B} envs in {eN:.1f} s); 1 thread: {v1:.4g} steps/s ({n1} steps)",
+            "spread": [round(r, 1) for r in rates]}
+
+
+def cpu_baselines_in_child(args):
+    """Both CPU baselines in a fresh child process that has never touched the
+    GPU and starts with this process's full CPU mask (its OpenMP and torch
+    thread pools are created there, so no pinning of this rank leaks into
+    them).  The parent waits for the child's JSON line."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--env", args.env,
+           "--hazards", str(args.hazards), "--cpu-seconds", str(args.cpu_seconds)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"CPU baseline child failed ({r.returncode}): {r.stderr[-2000:]}")
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
 
 
 def cpu_reference_mode(env_name, hazards, seconds):
@@ -244,21 +265,32 @@ class _DryRun:
 
 def pin_host_cores(local, n):
     """Keep this rank's host threads (the replay calls and the HIP runtime's
-    own threads, created after this) on n cores of their own, rank r on the
-    r-th group of the allowed CPUs, before anything touches the GPU.  The
-    replay call then takes 14-16 us instead of 18-34 us of host time in the
-    driver's 20-step form (profiles/r02/host_pinning_study_r02ag.txt).
-    Returns the original mask (restored for the CPU baseline), or None when
-    pinning is off or there are too few CPUs."""
+    own threads, created after this) on n cores of their own, before anything
+    touches the GPU (device counting included).  The replay call then takes
+    14-16 us instead of 18-34 us of host time in the driver's 20-step form
+    (profiles/r02/host_pinning_study_r02ag.txt).  The node's allowed CPUs are
+    split evenly over LOCAL_WORLD_SIZE ranks, each on its GPU's NUMA node
+    where the sysfs topology says which it is (rcbf_amd.shard.plan_host_cores:
+    every rank pinned, or none).  Returns (the original mask, this rank's
+    cores); the original mask is None when nothing was pinned.  The restore
+    before the CPU baseline covers the calling thread; the baseline's OpenMP
+    threads are created after it and inherit the full mask."""
+    from rcbf_amd import shard
     allowed = sorted(os.sched_getaffinity(0))
-    if n <= 0 or len(allowed) < n * (local + 1):
-        return None
-    os.sched_setaffinity(0, set(allowed[n * local:n * (local + 1)]))
-    return set(allowed)
+    plan = shard.plan_host_cores(allowed, shard.local_world_size(), n, shard.gpu_numa_nodes(), shard.node_cpus())
+    if plan is None or local >= len(plan):
+        return None, None
+    os.sched_setaffinity(0, set(plan[local]))
+    return set(allowed), plan[local]
 
 
 def main():
     args = parse()
+    if args.cpu_baseline_only:
+        print(json.dumps({"cpu_baseline": cpu_baseline(args.env, args.hazards, args.cpu_seconds),
+                          "cpu_reference_mode": cpu_reference_mode(args.env, args.hazards, args.cpu_seconds / 3)}),
+              flush=True)
+        return
     from rcbf_amd import shard
     rank, local, world = shard.world_info()
     if world == 1 and args.gpus > 1:
@@ -270,24 +302,24 @@ def main():
             raise SystemExit("--scaling strong needs --batch divisible by the GPU count")
         args.batch //= world
     B = args.batch
-    host_mask = None
+    host_mask = host_cores = None
     if args.cpu_dry_run:
         dev = torch.device("cpu")
         if world > 1:
             dist.init_process_group("gloo")
         S, reps = args.steps, 1
         graph = env = _DryRun(B, 1 if args.env == "SimulatedCars" else 2)
-        active_frac, layer = 0.0, None
+        active_frac, layer, untimed = 0.0, None, 0
         sync = lambda: None  # noqa: E731
     else:
+        host_mask, host_cores = pin_host_cores(local, args.host_cores)
         if local >= torch.cuda.device_count():
             raise SystemExit(f"rank {rank}: LOCAL_RANK {local}, but {torch.cuda.device_count()} HIP device(s) visible")
-        host_mask = pin_host_cores(local, args.host_cores)
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if world > 1:
             dist.init_process_group("nccl", device_id=dev)
-        env, layer, graph, S, active_frac = setup_gpu(args, dev, rank, B)
+        env, layer, graph, S, active_frac, untimed = setup_gpu(args, dev, rank, B)
         reps = args.steps // S
         sync = torch.cuda.synchronize
 
@@ -302,6 +334,7 @@ def main():
             graph.replay()
         ev1.record()
         sync()
+        untimed += reps * S
     shard.barrier(world)
     sync()
     t0 = time.perf_counter()
@@ -318,7 +351,8 @@ def main():
     # per fused-step launch, HIP events on the launch stream (torch's current stream)
     kern_ms = ev0.elapsed_time(ev1) / args.steps if not args.cpu_dry_run else 0.0
     env.check_failures()
-    el = shard.max_over_ranks(el, world, dev)
+    per_rank_s = shard.gather_over_ranks(el, world, dev)
+    el = max(per_rank_s)
     kern_ms = shard.max_over_ranks(kern_ms, world, dev)
     value = shard.whole_job_rate(world, B, args.steps, el)
     bps = bytes_per_step(args)
@@ -337,6 +371,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "untimed_steps_executed": untimed,
         "ms_per_step": round(el / args.steps * 1e3, 5),
         "higher_is_better": True,
         "scaling": args.scaling,
@@ -351,7 +386,7 @@ def main():
                    "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
                    "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)",
                    "prior": args.prior, "qp_active_frac_at_start": round(active_frac, 4),
-                   "host_cores_per_rank": args.host_cores if host_mask else None},
+                   "host_cores_per_rank": len(host_cores) if host_cores else None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
@@ -361,13 +396,16 @@ def main():
                                "region / steps (includes the graph launch and the inter-kernel gaps); host_submit_ms "
                                "= host time spent in the graph replay calls"},
     }
+    if world > 1:  # the spread of the timed region over ranks (value is set by the slowest)
+        ms = sorted(v / args.steps * 1e3 for v in per_rank_s)
+        rec["per_rank_ms"] = {"min": round(ms[0], 5), "median": round(float(np.median(ms)), 5),
+                              "max": round(ms[-1], 5)}
     if extra:
         rec["extra"] = extra
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.cpu_dry_run:
-        if host_mask:  # the CPU baseline gets every allowed core back
+        if host_mask:  # the child starts with every allowed core
             os.sched_setaffinity(0, host_mask)
-        rec["cpu_baseline"] = cpu_baseline(args.env, args.hazards, args.cpu_seconds)
-        rec["cpu_reference_mode"] = cpu_reference_mode(args.env, args.hazards, args.cpu_seconds / 3)
+        rec.update(cpu_baselines_in_child(args))
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
@@ -418,6 +456,7 @@ def setup_gpu(args, dev, rank, B):
 
     # fraction of envs whose safety filter changes the action at the start states
     steps(1)
+    untimed = 1 + max(args.warmup, 1)
     active_frac = float((outs["u"] != pool[0]).any(1).float().mean().item())
     # warmup (eager), then capture S fused steps into one hipGraph
     steps(max(args.warmup, 1))
@@ -428,6 +467,7 @@ def setup_gpu(args, dev, rank, B):
                 env.safe_step_seq(pool, layer, mean=mean, sigma=sigma, outputs=outs, steps=S)
         graph = _Seq()
         graph.replay()
+        untimed += S
     elif args.no_graph:
         class _Eager:
             def replay(self):
@@ -444,9 +484,10 @@ def setup_gpu(args, dev, rank, B):
             steps(S)
         for _ in range(2):
             graph.replay()
+        untimed += 2 + 2 * S
     torch.cuda.synchronize()
     env.check_failures()
-    return env, layer, graph, S, active_frac
+    return env, layer, graph, S, active_frac, untimed
 
 
 def sac_update_safe_action(env, layer, dev):

@@ -16,6 +16,8 @@
 
 #include <c10/hip/HIPStream.h>
 
+#include <cstring>
+
 #include "rcbf_hip.h"
 
 namespace {
@@ -62,7 +64,11 @@ struct SafeActionOp : public torch::autograd::Function<SafeActionOp> {
             }
         }
         ctx->save_for_backward({x, u, mu, sigma});
-        ctx->saved_data["prm"] = prm;
+        // the backward must not depend on the caller's layer object staying
+        // alive: keep a private copy of the parameter block with the graph
+        auto pcopy = torch::empty({(int64_t)sizeof(rcbf_params)}, torch::TensorOptions().dtype(torch::kUInt8));
+        std::memcpy(pcopy.data_ptr(), reinterpret_cast<const void*>(prm), sizeof(rcbf_params));
+        ctx->saved_data["prm"] = pcopy;
         ctx->saved_data["from_obs"] = from_obs;
         return out;
     }
@@ -72,10 +78,11 @@ struct SafeActionOp : public torch::autograd::Function<SafeActionOp> {
         auto saved = ctx->get_saved_variables();
         auto x = saved[0], u = saved[1], mu = saved[2], sigma = saved[3];
         const bool from_obs = ctx->saved_data["from_obs"].toBool();
-        const int64_t prm = ctx->saved_data["prm"].toInt();
+        const auto pcopy = ctx->saved_data["prm"].toTensor();
+        const auto* prm = reinterpret_cast<const rcbf_params*>(pcopy.data_ptr());
         auto g = grads[0].to(torch::kFloat32).contiguous();
         auto gu = torch::empty_like(u);
-        check_rc(g_bwd[from_obs ? 1 : 0](reinterpret_cast<const rcbf_params*>(prm), x.size(0), x.data_ptr<float>(),
+        check_rc(g_bwd[from_obs ? 1 : 0](prm, x.size(0), x.data_ptr<float>(),
                                          u.data_ptr<float>(), fptr(mu), fptr(sigma), g.data_ptr<float>(),
                                          gu.data_ptr<float>(), current_stream(x)),
                  from_obs ? "rcbf_obs_safe_action_backward" : "rcbf_safe_action_backward");

@@ -7,6 +7,7 @@ torch is imported first so the process has exactly one HIP runtime
 """
 import ctypes
 import os
+import warnings
 
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
@@ -142,10 +143,13 @@ def _bind_fast(lib):
     global _fast
     try:
         from . import _rcbf_fast
-    except ImportError:
+        _rcbf_fast.bind(*(entry_address(lib, n) for n in FAST_ENTRY_POINTS))
+    except (ImportError, AttributeError, TypeError) as e:
+        # not built, or a stale build without this bind(): the ctypes path serves
+        if not isinstance(e, ImportError):
+            warnings.warn(f"_rcbf_fast unusable ({e}); rebuild with `python __graft_entry__.py build`")
         _fast = None
         return
-    _rcbf_fast.bind(*(entry_address(lib, n) for n in FAST_ENTRY_POINTS))
     _fast = _rcbf_fast
 
 
@@ -160,10 +164,12 @@ def _bind_torch_op(lib):
     global _torch_op
     try:
         from . import _rcbf_torch
-    except ImportError:
+        _rcbf_torch.bind(*(entry_address(lib, n) for n in TORCH_OP_ENTRY_POINTS))
+    except (ImportError, AttributeError, TypeError) as e:
+        if not isinstance(e, ImportError):
+            warnings.warn(f"_rcbf_torch unusable ({e}); rebuild with `python __graft_entry__.py build`")
         _torch_op = None
         return
-    _rcbf_torch.bind(*(entry_address(lib, n) for n in TORCH_OP_ENTRY_POINTS))
     _torch_op = _rcbf_torch
 
 

@@ -56,3 +56,35 @@ def test_c_oracle_fused_step_matches_numpy():
         uo, rew, cost, done, fails = C.safe_step("Unicycle", xc, lc, sc, u, 20.0, hazards=hz, threads=2)
         assert fails == 0 and rel(uo, fin) <= 1e-5
         assert rel(xc, x) <= 1e-9
+
+
+@pytest.mark.parametrize("mode", ["SimulatedCars", "Unicycle"])
+def test_c_oracle_fused_step_with_mean_sigma_matches_numpy(mode):
+    """The C oracle's fused step with per-env mean/sigma (what the GPU parity
+    test of the post-GP-fit regime checks against) equals the numpy oracle,
+    which the reference fixtures pin with random mean/sigma."""
+    rng = np.random.default_rng(11)
+    B = 2048
+    hz = O.UNI["hazards"][:5] if mode == "Unicycle" else None
+    n_s = 10 if mode == "SimulatedCars" else 3
+    if mode == "SimulatedCars":
+        x, aux, st = O.cars_reset(rng.normal(0, 0.5, B))
+        st = rng.integers(0, 299, B)
+    else:
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        aux, st = O.uni_goal_dist(x), rng.integers(0, 999, B)
+    xc, ac, sc = x.copy(), aux.copy(), st.astype(np.int32)
+    for k in range(12):
+        u = rng.uniform(-1, 1, (B, 1 if mode == "SimulatedCars" else 2)).astype(np.float32)
+        mu = (0.01 * rng.normal(0, 1, (B, n_s))).astype(np.float32)
+        sg = (0.2 * rng.uniform(0, 1, (B, n_s)) + 0.05).astype(np.float32)
+        obs = O.cars_obs(x) if mode == "SimulatedCars" else O.uni_obs(x)
+        s32 = O.get_state_f32(mode, obs.astype(np.float32))
+        fin, _ = O.safe_action_diff(mode, s32, u, mu, sg, 20.0, hazards=hz)
+        if mode == "SimulatedCars":
+            x, aux, st, o, r, c, dn = O.cars_step(x, aux, st, fin)
+        else:
+            x, aux, st, o, r, c, dn, gm = O.uni_step(x, aux, st, fin, hazards=hz)
+        ref = C.safe_step_ex(mode, xc, ac, sc, u, 20.0, hazards=hz, mean=mu, sigma=sg, threads=2)
+        assert ref["fails"] == 0 and rel(ref["u"], fin) <= 1e-5
+        assert rel(xc, x) <= 1e-9 and np.array_equal(ref["cost"], np.asarray(c, np.float32))

@@ -69,14 +69,21 @@ def _worst(name, err, tol, extra=""):
     assert bad.size == 0, f"{name}: {bad.shape[0]} entries above {tol}, worst {err.max():.3e} at {bad[0]} {extra}"
 
 
-def run_teacher_forced(mode, B, steps, hazards=3, pool=8):
+def run_teacher_forced(mode, B, steps, hazards=3, pool=8, prior="prior"):
     """Run `steps` fused steps of bench's workload; compare each with the C
-    oracle started from the GPU's pre-step state.  Returns counts."""
+    oracle started from the GPU's pre-step state.  prior = "tensor": per-env
+    mean/sigma tensors (the post-GP-fit regime, generated as bench.py
+    --prior tensor does) passed to both.  Returns counts."""
     env, layer = _make(mode, B, hazards)
     gen = torch.Generator(device=env.device)
     gen.manual_seed(1000)
     bench.init_states(env, gen, mode)
     us = [(torch.rand(B, env.n_u, device=env.device, generator=gen) * 2 - 1).contiguous() for _ in range(pool)]
+    mean = sigma = mean_h = sigma_h = None
+    if prior == "tensor":  # bench.setup_gpu's post-GP-fit stand-in: small mean, sigma near MAX_STD
+        mean = (0.01 * torch.randn(B, env.n_s, device=env.device, generator=gen)).contiguous()
+        sigma = (0.2 * torch.rand(B, env.n_s, device=env.device, generator=gen) + 0.05).contiguous()
+        mean_h, sigma_h = mean.cpu().numpy(), sigma.cpu().numpy()
     outs = env.make_outputs()
     hz = env.hazards_locations if mode == "Unicycle" else None
     idx = env.env_offset + np.arange(B)
@@ -84,11 +91,12 @@ def run_teacher_forced(mode, B, steps, hazards=3, pool=8):
     for k in range(steps):
         x, aux, st, ep = _snapshot(env)
         u = us[k % pool]
-        env.safe_step(u, layer, outputs=outs)
+        env.safe_step(u, layer, mean=mean, sigma=sigma, outputs=outs)
         torch.cuda.synchronize()
         u_h = u.cpu().numpy()
         noise = 0.5 * O.normal_draw(env._rng_seed(), idx, ep + 1) if mode == "SimulatedCars" else None
-        ref = C.safe_step_ex(mode, x, aux, st, u_h, 20.0, hazards=hz, auto_reset=True, reset_noise=noise)
+        ref = C.safe_step_ex(mode, x, aux, st, u_h, 20.0, hazards=hz, mean=mean_h, sigma=sigma_h, auto_reset=True,
+                             reset_noise=noise)
         assert ref["fails"] == 0
         env.check_failures()
         tag = f"{mode} B={B} step {k}"
@@ -132,6 +140,23 @@ def test_headline_cars_B65536_vs_oracle():
 @pytest.mark.parametrize("k", [3, 5])
 def test_headline_unicycle_B65536_vs_oracle(k):
     r = run_teacher_forced("Unicycle", 65536, 24, hazards=k)
+    assert r["resets"] > 500
+    assert r["filter_active"] > 0.02 * r["env_steps"]
+
+
+def test_headline_cars_B65536_tensor_prior_vs_oracle():
+    """The post-GP-fit regime (dynamics.py:371-380 feeding the robust terms,
+    diff_cbf_qp.py:298-299): per-env sigma[5, 7, 9] read by the fused step."""
+    r = run_teacher_forced("SimulatedCars", 65536, 24, prior="tensor")
+    assert r["resets"] > 2000
+    assert r["filter_active"] > 0.05 * r["env_steps"]
+
+
+@pytest.mark.parametrize("k", [3, 5])
+def test_headline_unicycle_B65536_tensor_prior_vs_oracle(k):
+    """The post-GP-fit regime for the unicycle: per-env mu and sigma enter
+    the hazard rows (diff_cbf_qp.py:241, 261)."""
+    r = run_teacher_forced("Unicycle", 65536, 24, hazards=k, prior="tensor")
     assert r["resets"] > 500
     assert r["filter_active"] > 0.02 * r["env_steps"]
 

@@ -708,6 +708,44 @@ def test_torch_op_matches_python_function(mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["SimulatedCars", "Unicycle"])
+def test_torch_op_backward_outlives_the_layer(mode):
+    """The autograd graph keeps its own copy of the layer's parameter block
+    (csrc/rcbf_torch_op.cpp): a loss built with a temporary CBFQPLayer that is
+    dropped (and its memory reused) before loss.backward() still gives the
+    gradient of a live layer, bit for bit."""
+    import ctypes
+    import gc
+    from rcbf_amd import _lib
+    assert _lib.torch_op() is not None, "_rcbf_torch not built (run __graft_entry__.build())"
+    rng = np.random.default_rng(21)
+    B = 1024
+    hz = O.UNI["hazards"][:3] if mode == "Unicycle" else None
+    env = _env(mode, hz)
+    if mode == "SimulatedCars":
+        x, _, _ = _cars_states(B, 6)
+        s32 = O.get_state_f32(mode, O.cars_obs(x).astype(np.float32))
+    else:
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        s32 = O.get_state_f32(mode, O.uni_obs(x).astype(np.float32))
+    mu, sg = (dev(v.astype(np.float32)) for v in O.predict_disturbance_prior(mode, B))
+    u = rng.uniform(-1, 1, (B, env.n_u)).astype(np.float32)
+    w = dev(rng.normal(0, 1, (B, env.n_u)))
+    keep = _layer(env, 20.0)
+    a = dev(u).requires_grad_(True)
+    (keep.get_safe_action(dev(s32), a, mu, sg) * w).sum().backward()
+    tmp = _layer(env, 20.0)
+    b = dev(u).requires_grad_(True)
+    loss = (tmp.get_safe_action(dev(s32), b, mu, sg) * w).sum()
+    del tmp
+    gc.collect()
+    junk = [(ctypes.c_ubyte * ctypes.sizeof(_lib.RcbfParams))(*([0xFF] * ctypes.sizeof(_lib.RcbfParams)))
+            for _ in range(64)]
+    loss.backward()
+    del junk
+    assert torch.equal(a.grad, b.grad)
+
+
+@pytest.mark.parametrize("mode", ["SimulatedCars", "Unicycle"])
 @pytest.mark.parametrize("B", [1, 7, 256, 300])
 def test_env_step_sync_matches_device_step(mode, B):
     """rcbf_env_step_sync (the gym env.step path, main.py:95): action read

@@ -130,3 +130,66 @@ def test_bench_under_torchrun_launcher(n):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == n and rec["config"]["global_batch"] == n * 512
     assert rec["config"]["parallelism"] == f"env-shard x{n} (no collective)"
+    spread = rec["per_rank_ms"]  # the slowest rank sets value; the spread shows a straggler
+    assert spread["min"] <= spread["median"] <= spread["max"] == rec["ms_per_step"]
+
+
+def _check_plan(plan, world, cpus):
+    assert plan is not None and len(plan) == world
+    sizes = {len(m) for m in plan}
+    assert len(sizes) == 1 and sizes.pop() >= 1  # equal-sized
+    flat = [c for m in plan for c in m]
+    assert len(flat) == len(set(flat))  # disjoint
+    assert set(flat) <= set(cpus)
+
+
+@pytest.mark.parametrize("ncpu", [16, 64])
+@pytest.mark.parametrize("numa", [False, True])
+def test_host_core_plan_eight_ranks(ncpu, numa):
+    """bench.py --host-cores on an 8-GPU node: the allowed CPUs are split into
+    disjoint, equal-sized masks over the 8 local ranks (every rank pinned, or
+    none); with a 2-socket topology (GPUs 0-3 on node 0, 4-7 on node 1) each
+    rank's cores sit on its GPU's node."""
+    from rcbf_amd import shard
+    cpus = list(range(ncpu))
+    gpu_numa = [0, 0, 0, 0, 1, 1, 1, 1] if numa else []
+    node_cpus = {0: cpus[:ncpu // 2], 1: cpus[ncpu // 2:]} if numa else {}
+    plan = shard.plan_host_cores(cpus, 8, 4, gpu_numa, node_cpus)
+    _check_plan(plan, 8, cpus)
+    assert len(plan[0]) == min(4, ncpu // 8)
+    if numa:
+        for r in range(8):
+            assert set(plan[r]) <= set(node_cpus[gpu_numa[r]])
+    # a rank's GPU on a node with no allowed CPUs: fall back to the plain split, still equal and disjoint
+    plan = shard.plan_host_cores(cpus, 8, 4, [0] * 7 + [3], {0: cpus})
+    _check_plan(plan, 8, cpus)
+    # fewer CPUs than ranks: nobody is pinned
+    assert shard.plan_host_cores(cpus[:7], 8, 4) is None
+    assert shard.plan_host_cores(cpus, 8, 0) is None
+
+
+def test_gpu_numa_nodes_from_a_sysfs_tree(tmp_path, monkeypatch):
+    """The GPU -> NUMA node map is read from the KFD topology and the PCI
+    devices' numa_node (no GPU call), CPU nodes skipped, visible-device masks
+    applied."""
+    from rcbf_amd import shard
+    topo = tmp_path / "class/kfd/kfd/topology/nodes"
+    gpus = [(0x0300, 0), (0x8300, 1)]  # (location_id, numa node): bus 03 and bus 83
+    (topo / "0").mkdir(parents=True)
+    (topo / "0/properties").write_text("cpu_cores_count 64\nsimd_count 0\n")
+    for k, (loc, node) in enumerate(gpus, 1):
+        (topo / str(k)).mkdir()
+        (topo / str(k) / "properties").write_text(f"simd_count 1024\nlocation_id {loc}\ndomain 0\n")
+        bdf = tmp_path / "bus/pci/devices" / f"0000:{loc >> 8:02x}:00.0"
+        bdf.mkdir(parents=True)
+        (bdf / "numa_node").write_text(f"{node}\n")
+    for n, cl in ((0, "0-3,8-11"), (1, "4-7,12-15")):
+        (tmp_path / f"devices/system/node/node{n}").mkdir(parents=True)
+        (tmp_path / f"devices/system/node/node{n}/cpulist").write_text(cl + "\n")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    assert shard.gpu_numa_nodes(str(tmp_path)) == [0, 1]
+    assert shard.node_cpus(str(tmp_path)) == {0: [0, 1, 2, 3, 8, 9, 10, 11], 1: [4, 5, 6, 7, 12, 13, 14, 15]}
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert shard.gpu_numa_nodes(str(tmp_path)) == [1]
+    assert shard.gpu_numa_nodes(str(tmp_path / "nowhere")) == []
