@@ -26,7 +26,7 @@ def lib():
         _lib.oracle_safe_step.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double, ctypes.c_int64,
                                           P, P, P, P, P, P, P, P, ctypes.c_int]
         _lib.oracle_safe_step_ex.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double, ctypes.c_int64,
-                                             P, P, P, P, P, P, P, P, P, P, P, P, ctypes.c_int, P, ctypes.c_int]
+                                             P, P, P, P, P, P, P, P, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int]
         _lib.oracle_max_threads.restype = ctypes.c_int
     return _lib
 
@@ -67,10 +67,12 @@ def safe_step(mode, x, aux, step, u, gamma_b, hazards=None, threads=0):
 
 
 def safe_step_ex(mode, x, aux, step, u, gamma_b, hazards=None, mean=None, sigma=None, auto_reset=False,
-                 reset_noise=None, threads=0):
+                 reset_noise=None, env_action=None, threads=0):
     """In-place fused step with the kernel's full output set: mean/sigma
     (B, n_s) f32 or None (prior), auto-reset with the cars reset draw injected
     (reset_noise (B,) f64 = the N(0, 0.5) sample an env takes if it resets).
+    env_action (B, n_u) f32 or None: step the env with this action instead of
+    the oracle's own safe action (still returned as "u").
     Returns dict(u, reward, cost, done, goal, obs, fails)."""
     m = 0 if mode == "SimulatedCars" else 1
     n_o = 10 if m == 0 else 7
@@ -81,6 +83,7 @@ def safe_step_ex(mode, x, aux, step, u, gamma_b, hazards=None, mean=None, sigma=
     mu = None if mean is None else np.ascontiguousarray(mean, np.float32)
     sg = None if sigma is None else np.ascontiguousarray(sigma, np.float32)
     nz = None if reset_noise is None else np.ascontiguousarray(reset_noise, np.float64)
+    ea = None if env_action is None else np.ascontiguousarray(env_action, np.float32).reshape(u.shape)
     out = dict(u=np.empty_like(u), reward=np.empty(B, np.float32), cost=np.empty(B, np.float32),
                done=np.empty(B, np.uint8), goal=np.empty(B, np.uint8), obs=np.empty((B, n_o), np.float32))
 
@@ -89,7 +92,7 @@ def safe_step_ex(mode, x, aux, step, u, gamma_b, hazards=None, mean=None, sigma=
     out["fails"] = lib().oracle_safe_step_ex(m, K, _p(hz), float(gamma_b), B, _p(x), _p(aux), _p(step), _p(u),
                                              pp(mu), pp(sg), _p(out["u"]), _p(out["reward"]), _p(out["cost"]),
                                              _p(out["done"]), _p(out["goal"]), _p(out["obs"]), int(auto_reset),
-                                             pp(nz), int(threads))
+                                             pp(nz), pp(ea), int(threads))
     return out
 
 

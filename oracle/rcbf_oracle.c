@@ -335,11 +335,14 @@ static void uni_obs32(const double* xs, float* o) {
  * auto_reset a finished env is reset (simulated_cars_env.py:108-125 /
  * unicycle_env.py:125-143) and its obs is that of the reset state.  The cars
  * reset velocity draw is injected (reset_noise[i] = the N(0, 0.5) sample,
- * NULL -> 0).  obs_out / goal_out may be NULL. */
+ * NULL -> 0).  obs_out / goal_out may be NULL.  env_action (may be NULL): the
+ * action the env steps with instead of the oracle's own safe action (which
+ * u_out still reports) -- the parity tests step the oracle env with the
+ * device's action, so the env physics is checked exactly on its own. */
 int oracle_safe_step_ex(int mode, int K, const double* hz, double gamma_b, int64_t B, double* x, double* aux,
                         int32_t* step, const float* u, const float* mu_in, const float* sig_in, float* u_out,
                         float* rew, float* cost, uint8_t* done, uint8_t* goal_out, float* obs_out, int auto_reset,
-                        const double* reset_noise, int nthreads) {
+                        const double* reset_noise, const float* env_action, int nthreads) {
     int fails = 0;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -363,6 +366,7 @@ int oracle_safe_step_ex(int mode, int K, const double* hz, double gamma_b, int64
             float v = u[i] + (float)z[0];
             float a = fminf(fmaxf(v, -10.0f), 10.0f);
             u_out[i] = a;
+            if (env_action) a = env_action[i];
             cars_env(xs, aux + i, step + i, a, rew + i, cost + i, done + i);
             if (goal_out) goal_out[i] = 0;
             if (auto_reset && done[i]) {
@@ -393,6 +397,7 @@ int oracle_safe_step_ex(int mode, int K, const double* hz, double gamma_b, int64
                 float v = u[2 * i + c] + (float)z[c];
                 a[c] = fminf(fmaxf(v, -2.5f), 2.5f);
                 u_out[2 * i + c] = a[c];
+                if (env_action) a[c] = env_action[2 * i + c];
             }
             uni_env(xs, aux + i, step + i, a, K, hz, rew + i, cost + i, done + i);
             if (goal_out) goal_out[i] = goal_dist(xs) <= 0.3;
@@ -412,7 +417,7 @@ int oracle_safe_step(int mode, int K, const double* hz, double gamma_b, int64_t 
                      int32_t* step, const float* u, float* u_out, float* rew, float* cost, uint8_t* done,
                      int nthreads) {
     return oracle_safe_step_ex(mode, K, hz, gamma_b, B, x, aux, step, u, NULL, NULL, u_out, rew, cost, done, NULL,
-                               NULL, 0, NULL, nthreads);
+                               NULL, 0, NULL, NULL, nthreads);
 }
 
 int oracle_max_threads(void) {

@@ -8,6 +8,12 @@
 
 #include "rcbf_device.hpp"
 
+// The fused step solves the raw CBF rows (layer_forward's RAW); 0 restores
+// the normalised rows (the A/B build of the study).
+#ifndef RCBF_FUSED_RAW_ROWS
+#define RCBF_FUSED_RAW_ROWS 1
+#endif
+
 namespace rcbf {
 
 constexpr int kBlock = 256;
@@ -183,13 +189,36 @@ struct LayerState {
 // build -> normalise -> fp64 QP -> .float() -> clamp.
 // NEED_LAM: the caller needs the multipliers and the active set (backward);
 // otherwise the cars path uses the 1-D exact solver (cars_qp_1d).
-template <int SOLVER, int MODE, int K, bool NEED_LAM = false, bool ST = false>
+// RAW (the fused safe step, exact solver only): the rows are solved as built,
+// without the row normalisation -- a positive scaling of each row that the
+// exact optimum does not depend on (cars_qp_1d_raw); L.G / L.h then hold the
+// raw rows and L.Nrm / L.ish are not set.
+template <int SOLVER, int MODE, int K, bool NEED_LAM = false, bool ST = false, bool RAW = false>
 __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const float* xs, const float* u,
                                               const float* mu, const float* sig, float* u_final,
                                               LayerState<MODE, K>& L, const Stamps<ST>& stamps = {},
                                               const float* cs_row = nullptr) {
     using D = Dims<MODE, K>;
     diff_rows<MODE, K>(prm, xs, u, mu, sig, L.G, L.h, cs_row);
+    if constexpr (RAW && SOLVER == RCBF_SOLVER_ACTIVE_SET && !NEED_LAM) {
+        stamps.mark(3, false);
+        PMat<D::N, true> pm;
+        double pd[D::N];
+        diff_P<MODE>(pd);
+        pmat_set_diag<D::N>(pm, pd);
+        if constexpr (MODE == RCBF_MODE_SIMULATED_CARS)
+            cars_qp_1d_raw<float>(pm, L.G, L.h, L.qp.z, L.qp.status);
+        else
+            uni_qp_2d_raw<K, float>(pm, L.G, L.h, L.qp.z, L.qp.status);
+        stamps.mark(4, false);
+#pragma unroll
+        for (int c = 0; c < D::NU; ++c) {
+            float v = u[c] + (float)L.qp.z[c];
+            float lo = (float)prm.u_min[c], hi = (float)prm.u_max[c];
+            u_final[c] = fminf(fmaxf(v, lo), hi);  // torch.clamp (diff_cbf_qp.py:77)
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < D::M; ++r) {
         L.hraw[r] = L.h[r];
@@ -309,8 +338,8 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
     }
     stamps.mark(2, false);
     LayerState<MODE, K> L;
-    layer_forward<SOLVER, MODE, K, false, ST>(prm, s32, us, m, s, uf, L, stamps,
-                                              MODE == RCBF_MODE_UNICYCLE ? cs_row : nullptr);
+    layer_forward<SOLVER, MODE, K, false, ST, RCBF_FUSED_RAW_ROWS != 0>(prm, s32, us, m, s, uf, L, stamps,
+                                                                       MODE == RCBF_MODE_UNICYCLE ? cs_row : nullptr);
     status = L.qp.status;
     stamps.count(9, uf[0] != us[0]);  // lanes whose action the filter changed
     if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {

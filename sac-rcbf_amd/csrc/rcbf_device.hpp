@@ -1135,6 +1135,52 @@ __device__ __forceinline__ void cars_qp_1d(const PMat<2, true>& pm, const R (*G)
     if (!fin) z[0] = z[1] = __builtin_nan("");
 }
 
+// The same exact solver on the cars layer's RAW rows (the fused safe step):
+// the reference row-normalises before qpth (diff_cbf_qp.py:103-106), a
+// positive scaling of each row that leaves the feasible set, hence the
+// exact optimum, unchanged -- so the fused step skips it and solves the rows
+// as built.  Rows 0, 1: G_r0 u + G_r1 eps <= h_r with G_r1 = -200 exactly
+// (cars_rows_diff); rows 2, 3: u <= h_2, -u <= h_3.  With eps' = 200 eps the
+// CBF rows read eps' >= e_r(u) = G_r0 u - h_r and the slack weight is
+// p1 / 40000, so e_r's coefficients are the fp32 row entries themselves (no
+// division) and the actuator bounds are h_2 and -h_3.  Against the
+// normalised problem the optimum moves only by the fp32 rounding of the
+// normalised entries (~1e-7 relative), far inside the north star's 1e-4.
+template <typename R>
+__device__ __forceinline__ void cars_qp_1d_raw(const PMat<2, true>& pm, const R (*G)[2], const R* h, double* z,
+                                               int& status) {
+    const double p0 = pm.P[0][0], p1 = pm.P[1][1] * (1.0 / 40000.0);
+    const double a0 = (double)G[0][0], b0 = -(double)h[0];
+    const double a1 = (double)G[1][0], b1 = -(double)h[1];
+    const double U = (double)h[2], L = -(double)h[3];
+    const double c1 = -(p1 * a0 * b0) * rcp64_qp_nz(fma(p1 * a0, a0, p0));
+    const double c2 = -(p1 * a1 * b1) * rcp64_qp_nz(fma(p1 * a1, a1, p0));
+    const double den = a0 - a1;
+    const double c3 = (den != 0.0) ? (b1 - b0) * rcp64_qp_nz(den) : 0.0;
+    auto clampu = [&](double u) { return fmin(fmax(u, L), U); };
+    auto phi = [&](double u) {
+        double e = fmax(0.0, fmax(fma(a0, u, b0), fma(a1, u, b1)));
+        return fma(p0 * u, u, p1 * e * e);
+    };
+    double ub = clampu(0.0), fb = phi(ub);
+    double u1 = clampu(c1), f1 = phi(u1);
+    double u2 = clampu(c2), f2 = phi(u2);
+    double u3 = clampu(c3), f3 = phi(u3);
+    ub = (f1 < fb) ? u1 : ub;
+    fb = fmin(f1, fb);
+    ub = (f2 < fb) ? u2 : ub;
+    fb = fmin(f2, fb);
+    ub = (f3 < fb) ? u3 : ub;
+    z[0] = ub;
+    z[1] = fmax(0.0, fmax(fma(a0, ub, b0), fma(a1, ub, b1))) * (1.0 / 200.0);
+    // non-finite rows are caught on the inputs (fmin/fmax drop NaNs); the
+    // reference's solver returns NaN there and the layer raises (:141-143)
+    const bool fin = isfinite(a0 + b0 + a1 + b1 + U + L + (double)G[0][1] + (double)G[1][1]);
+    const bool ok = fin && isfinite(z[0]) && (L <= U);
+    status = ok ? RCBF_QP_OK : (fin ? RCBF_QP_INFEASIBLE : RCBF_QP_NONFINITE);
+    if (!fin) z[0] = z[1] = __builtin_nan("");
+}
+
 // Exact solver for the UNICYCLE QP structure (both formulations), z = (u0, u1, eps):
 //   rows j < K:  g_j0 u0 + g_j1 u1 + g_j2 eps <= h_j  with g_j2 < 0 (slack column)
 //   rows K..K+3: u0 <= U0, -u0 <= .., u1 <= U1, -u1 <= ..  (the actuator box)
@@ -1342,11 +1388,99 @@ __device__ __forceinline__ int wave_max_count(int cnt) {
     return kmax;
 }
 
+// Slots 0..KK-1 of a lane: its first KK live rows in row order (mask bit j =
+// row j live), compacted with selects (a lane-varying array index would be
+// turned into LDS traffic by the compiler); slots past its live count repeat
+// slot 0 (row 0 if none is live), which only adds NaN kink / triple
+// candidates that never win.
+template <int KK, int K, typename T>
+__device__ __forceinline__ void uni_slots_solve(double p0, double p1, double p2, double ip0, double ip1,
+                                                const T* a0, const T* a1, const T* b, unsigned mask, double L0,
+                                                double U0, double L1, double U1, double& bu0, double& bu1,
+                                                double& bf, double& e) {
+    T S0[KK], S1[KK], SB[KK];
+#pragma unroll
+    for (int s = 0; s < KK; ++s) {
+        S0[s] = a0[0];
+        S1[s] = a1[0];
+        SB[s] = b[0];
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const bool live = (mask >> j) & 1u;
+#pragma unroll
+        for (int s = 0; s < KK && s <= j; ++s) {  // row j can only land in slots 0..j
+            const bool here = live && (cnt == s);
+            S0[s] = here ? a0[j] : S0[s];
+            S1[s] = here ? a1[j] : S1[s];
+            SB[s] = here ? b[j] : SB[s];
+        }
+        cnt += live ? 1 : 0;
+    }
+    double A0[KK], A1[KK], Bv[KK];
+#pragma unroll
+    for (int s = 0; s < KK; ++s) {  // unused slots repeat slot 0
+        A0[s] = (double)((s == 0 || s < cnt) ? S0[s] : S0[0]);
+        A1[s] = (double)((s == 0 || s < cnt) ? S1[s] : S1[0]);
+        Bv[s] = (double)((s == 0 || s < cnt) ? SB[s] : SB[0]);
+    }
+    uni_pieces_solve<KK>(p0, p1, p2, ip0, ip1, A0, A1, Bv, L0, U0, L1, U1, bu0, bu1, bf);
+    // eps at the optimum: the live rows' max (a dropped row has e_j <= 0 on the whole box)
+    e = 0.0;
+#pragma unroll
+    for (int s = 0; s < KK; ++s) e = fmax(e, fma(A0[s], bu0, fma(A1[s], bu1, Bv[s])));
+}
+
+// The 2-D solve from the slack form: eps >= e_j(u) = a0_j u0 + a1_j u1 + b_j
+// for the K hazard rows (T: float for the raw fp32 rows, double otherwise),
+// the box [L0, U0] x [L1, U1]; finite: the caller's check of its inputs.
+// Live rows (max over the box of e_j > 0; NaN data keeps the row, and such a
+// lane fails below anyway) form a per-lane bit mask; the wave solves with KK
+// = the largest live count of its lanes, picking only KK slots per lane.
+template <int K, typename T>
+__device__ __forceinline__ void uni_qp_2d_core(double p0, double p1, double p2, double ip0, double ip1,
+                                               const T* a0, const T* a1, const T* b, double L0, double U0,
+                                               double L1, double U1, bool finite, double* z, int& status) {
+    unsigned mask = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const double x0 = (double)a0[j], x1 = (double)a1[j];
+        const double emax = (double)b[j] + fmax(x0 * L0, x0 * U0) + fmax(x1 * L1, x1 * U1);
+        mask |= (emax <= 0.0 ? 0u : 1u) << j;
+    }
+    double bu0, bu1, bf, e;
+    const int kmax = wave_max_count<K>(__popc(mask));
+    if (kmax == 0) {  // no hazard row can bind anywhere in the box, for every lane of the wave
+        bu0 = fmin(fmax(0.0, L0), U0);
+        bu1 = fmin(fmax(0.0, L1), U1);
+        bf = 0.0;
+        e = 0.0;
+    } else if (kmax == 1 || K == 1) {
+        uni_slots_solve<1, K, T>(p0, p1, p2, ip0, ip1, a0, a1, b, mask, L0, U0, L1, U1, bu0, bu1, bf, e);
+    } else if (kmax == 2 || K == 2) {
+        uni_slots_solve<(K >= 2 ? 2 : 1), K, T>(p0, p1, p2, ip0, ip1, a0, a1, b, mask, L0, U0, L1, U1, bu0, bu1,
+                                                bf, e);
+    } else if (kmax == 3 || K == 3) {
+        uni_slots_solve<(K >= 3 ? 3 : 1), K, T>(p0, p1, p2, ip0, ip1, a0, a1, b, mask, L0, U0, L1, U1, bu0, bu1,
+                                                bf, e);
+    } else {
+        uni_slots_solve<K, K, T>(p0, p1, p2, ip0, ip1, a0, a1, b, mask, L0, U0, L1, U1, bu0, bu1, bf, e);
+    }
+    z[0] = bu0;
+    z[1] = bu1;
+    z[2] = e;
+    finite = finite && isfinite(U0 + L0 + U1 + L1);  // fmin/fmax would hide a NaN bound
+    const bool ok = isfinite(z[0]) && isfinite(z[1]) && isfinite(z[2]) && bf < __builtin_huge_val();
+    status = !finite ? RCBF_QP_NONFINITE : (ok && L0 <= U0 && L1 <= U1 ? RCBF_QP_OK : RCBF_QP_INFEASIBLE);
+    if (!finite) z[0] = z[1] = z[2] = __builtin_nan("");
+}
+
+// On the normalised rows (what qpth sees): back to the slack form by one
+// division per row by its (negative) slack coefficient.
 template <int K, typename R>
 __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[3], const R* h, double* z,
                                           int& status) {
-    const double p0 = pm.P[0][0], p1 = pm.P[1][1], p2 = pm.P[2][2];
-    const double ip0 = pm.Pinv[0][0], ip1 = pm.Pinv[1][1];
     double a0[K], a1[K], b[K];
     bool finite = true;
 #pragma unroll
@@ -1361,59 +1495,31 @@ __device__ __forceinline__ void uni_qp_2d(const PMat<3, true>& pm, const R (*G)[
     const double L0 = (double)h[K + 1] * rcp64_qp_nz((double)G[K + 1][0]);
     const double U1 = (double)h[K + 2] * rcp64_qp_nz((double)G[K + 2][1]);
     const double L1 = (double)h[K + 3] * rcp64_qp_nz((double)G[K + 3][1]);
-    // live rows: max over the box of e_j(u) > 0 (NaN data keeps the row; such a lane fails below anyway)
-    double A0[K], A1[K], Bv[K];
-    int cnt = 0;
-#pragma unroll
-    for (int s = 0; s < K; ++s) {
-        A0[s] = a0[0];
-        A1[s] = a1[0];
-        Bv[s] = b[0];
-    }
+    uni_qp_2d_core<K, double>(pm.P[0][0], pm.P[1][1], pm.P[2][2], pm.Pinv[0][0], pm.Pinv[1][1], a0, a1, b, L0, U0,
+                              L1, U1, finite, z, status);
+}
+
+// On the RAW rows (the fused safe step; see cars_qp_1d_raw for why the
+// normalisation can be skipped): hazard rows -a_j.u - eps <= h_j have slack
+// coefficient -1 exactly (uni_rows_diff_cs), so e_j(u) = G_j0 u0 + G_j1 u1
+// - h_j with the fp32 entries as they are, and the actuator rows are +-1:
+// U0 = h_K, L0 = -h_{K+1}, U1 = h_{K+2}, L1 = -h_{K+3}.  No division at all.
+template <int K, typename R>
+__device__ __forceinline__ void uni_qp_2d_raw(const PMat<3, true>& pm, const R (*G)[3], const R* h, double* z,
+                                              int& status) {
+    R a0[K], a1[K], b[K];
+    double chk = 0.0;  // NaN / inf in any entry makes the sum non-finite (fp32 inputs cannot overflow it)
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        const double emax = b[j] + fmax(a0[j] * L0, a0[j] * U0) + fmax(a1[j] * L1, a1[j] * U1);
-        const bool live = !(emax <= 0.0);
-#pragma unroll
-        for (int s = 0; s <= j; ++s) {  // row j can only land in slots 0..j
-            const bool here = live && (cnt == s);
-            A0[s] = here ? a0[j] : A0[s];
-            A1[s] = here ? a1[j] : A1[s];
-            Bv[s] = here ? b[j] : Bv[s];
-        }
-        cnt += live ? 1 : 0;
+        a0[j] = G[j][0];
+        a1[j] = G[j][1];
+        b[j] = -h[j];  // exact
+        chk += ((double)a0[j] + (double)a1[j]) + ((double)b[j] + (double)G[j][2]);
     }
-#pragma unroll
-    for (int s = 1; s < K; ++s) {  // unused slots repeat slot 0
-        A0[s] = (s < cnt) ? A0[s] : A0[0];
-        A1[s] = (s < cnt) ? A1[s] : A1[0];
-        Bv[s] = (s < cnt) ? Bv[s] : Bv[0];
-    }
-    double bu0, bu1, bf;
-    const int kmax = wave_max_count<K>(cnt);
-    if (kmax == 0) {  // no hazard row can bind anywhere in the box, for every lane of the wave
-        bu0 = fmin(fmax(0.0, L0), U0);
-        bu1 = fmin(fmax(0.0, L1), U1);
-        bf = 0.0;
-    } else if (kmax == 1 || K == 1) {
-        uni_pieces_solve<1>(p0, p1, p2, ip0, ip1, A0, A1, Bv, L0, U0, L1, U1, bu0, bu1, bf);
-    } else if (kmax == 2 || K == 2) {
-        uni_pieces_solve<(K >= 2 ? 2 : 1)>(p0, p1, p2, ip0, ip1, A0, A1, Bv, L0, U0, L1, U1, bu0, bu1, bf);
-    } else if (kmax == 3 || K == 3) {
-        uni_pieces_solve<(K >= 3 ? 3 : 1)>(p0, p1, p2, ip0, ip1, A0, A1, Bv, L0, U0, L1, U1, bu0, bu1, bf);
-    } else {
-        uni_pieces_solve<K>(p0, p1, p2, ip0, ip1, A0, A1, Bv, L0, U0, L1, U1, bu0, bu1, bf);
-    }
-    z[0] = bu0;
-    z[1] = bu1;
-    double e = 0.0;  // eps at the optimum over ALL rows (the dropped ones are <= 0 there)
-#pragma unroll
-    for (int j = 0; j < K; ++j) e = fmax(e, fma(a0[j], bu0, fma(a1[j], bu1, b[j])));
-    z[2] = e;
-    finite = finite && isfinite(U0 + L0 + U1 + L1);  // fmin/fmax would hide a NaN bound
-    const bool ok = isfinite(z[0]) && isfinite(z[1]) && isfinite(z[2]) && bf < __builtin_huge_val();
-    status = !finite ? RCBF_QP_NONFINITE : (ok && L0 <= U0 && L1 <= U1 ? RCBF_QP_OK : RCBF_QP_INFEASIBLE);
-    if (!finite) z[0] = z[1] = z[2] = __builtin_nan("");
+    const double U0 = (double)h[K], L0 = -(double)h[K + 1];
+    const double U1 = (double)h[K + 2], L1 = -(double)h[K + 3];
+    uni_qp_2d_core<K, R>(pm.P[0][0], pm.P[1][1], pm.P[2][2], pm.Pinv[0][0], pm.Pinv[1][1], a0, a1, b, L0, U0, L1,
+                         U1, isfinite(chk), z, status);
 }
 
 // Compile-time solver choice (the host dispatches on rcbf_params.solver):

@@ -6,7 +6,9 @@ same pre-step state ("teacher forcing": each step is compared from identical
 inputs, so a difference cannot hide behind trajectory divergence).
 
 Per step, per env (north star: safe action within 1e-4 relative):
-  * safe action u:       |du| <= 1e-4 max(1, |u|)
+  * safe action u:       |du| <= 1e-4 max(1, |u|) against the oracle's own
+    safe action; the oracle env then steps with the DEVICE's action, so
+    everything below checks the env physics exactly on its own
   * env state, aux, step: <= 1e-9 relative (exact for step), except the
     velocities of a cars env that auto-reset in this step: the reset draw is
     0.5 * Box-Muller(Philox4x32-10(seed, global env, episode)) with the
@@ -95,8 +97,10 @@ def run_teacher_forced(mode, B, steps, hazards=3, pool=8, prior="prior"):
         torch.cuda.synchronize()
         u_h = u.cpu().numpy()
         noise = 0.5 * O.normal_draw(env._rng_seed(), idx, ep + 1) if mode == "SimulatedCars" else None
+        # the oracle's safe action vs the device's (1e-4); the oracle env then steps with the DEVICE's
+        # action, so the env physics, observations and resets are checked exactly on their own
         ref = C.safe_step_ex(mode, x, aux, st, u_h, 20.0, hazards=hz, mean=mean_h, sigma=sigma_h, auto_reset=True,
-                             reset_noise=noise)
+                             reset_noise=noise, env_action=outs["u"].cpu().numpy())
         assert ref["fails"] == 0
         env.check_failures()
         tag = f"{mode} B={B} step {k}"

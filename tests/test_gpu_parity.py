@@ -327,8 +327,9 @@ def test_fused_safe_step_cars(solver):
         s32 = O.get_state_f32("SimulatedCars", O.cars_obs(x).astype(np.float32))
         mu, sg = O.predict_disturbance_prior("SimulatedCars", B)
         fin, aux = O.safe_action_diff("SimulatedCars", s32, u, mu.astype(np.float32), sg.astype(np.float32), 20.0)
-        assert rel(out["u"].cpu().numpy(), fin) <= 1e-4
-        x, t, st, o, r, c, dn = O.cars_step(x, t, st, fin)
+        ug = out["u"].cpu().numpy()
+        assert rel(ug, fin) <= 1e-4
+        x, t, st, o, r, c, dn = O.cars_step(x, t, st, ug)  # the env physics, given the device's action
         assert rel(env.state_numpy(), x) <= 1e-9
         assert rel(obs.cpu().numpy(), o.astype(np.float32)) <= 1e-6
         assert rel(rew.cpu().numpy(), r) <= 1e-6
@@ -356,8 +357,9 @@ def test_fused_safe_step_unicycle(k):
         s32 = O.get_state_f32("Unicycle", O.uni_obs(x).astype(np.float32))
         fin, aux = O.safe_action_diff("Unicycle", s32, u, np.zeros((B, 3), np.float32),
                                       np.full((B, 3), 0.2, np.float32), 20.0, hazards=hz)
-        assert rel(out["u"].cpu().numpy(), fin) <= 1e-4
-        x, ld, st, o, r, c, dn, gm = O.uni_step(x, ld, st, fin, hazards=hz)
+        ug = out["u"].cpu().numpy()
+        assert rel(ug, fin) <= 1e-4
+        x, ld, st, o, r, c, dn, gm = O.uni_step(x, ld, st, ug, hazards=hz)  # the env physics, given the device's action
         assert rel(env.state_numpy(), x) <= 1e-9
         assert rel(rew.cpu().numpy(), r) <= 1e-5
     env.check_failures()
