@@ -351,7 +351,7 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
         gm = false;
     } else {
         UniStepOut o;
-        uni_env_step_cs<float>(prm, xs, a, st, uf, c_th, s_th, o);
+        uni_env_step_cs<float, K>(prm, xs, a, st, uf, c_th, s_th, o);
         rew = (float)o.reward;
         cst = (float)o.cost;
         dn = o.done;

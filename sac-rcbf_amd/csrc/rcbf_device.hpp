@@ -1986,7 +1986,10 @@ struct UniStepOut {
 // UnicycleEnv.step/_step (unicycle_env.py:46-111): clip to +-1 after the
 // safety filter, Euler step with g(x), then the -(dt*0.1) g(x') [cos th', 0]
 // drift evaluated left to right (:87).
-template <typename A>
+// KH > 0: the hazard count known at compile time (the fused step; the cost
+// test unrolls and reuses the hazard positions the rows already loaded,
+// instead of a loop of dependent scalar loads); 0: prm.num_hazards.
+template <typename A, int KH = 0>
 __device__ __forceinline__ void uni_env_step_cs(const rcbf_params& prm, double* xs, double& last_dist, int& step,
                                                 const A* action, double c, double s, UniStepOut& o) {
 #pragma clang fp contract(off)
@@ -2019,7 +2022,9 @@ __device__ __forceinline__ void uni_env_step_cs(const rcbf_params& prm, double* 
     o.reward = reward;
     bool hit = false;
     const double r2 = prm.hazards_radius * prm.hazards_radius;
-    for (int j = 0; j < prm.num_hazards; ++j) {
+    const int nh = KH > 0 ? KH : prm.num_hazards;
+#pragma unroll
+    for (int j = 0; j < nh; ++j) {
         double ex = xs[0] - prm.hazards_xy[2 * j], ey = xs[1] - prm.hazards_xy[2 * j + 1];
         hit = hit || (ex * ex + ey * ey < r2);
     }

@@ -295,9 +295,9 @@ int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, in
     if (!x || !aux || !step || !u_rl || !obs_out || !u_out || !reward || !cost || !done) return RCBF_E_NULL;
     if ((((uintptr_t)obs_out) & 7) || (((uintptr_t)x) & 15)) return RCBF_E_BAD_SHAPE;  // 8/16-B accesses
     RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0,
-                                          stream, *prm, B, x, aux, step, episode, u_rl, mu, sigma, obs_out, u_out,
-                                          reward, cost, done, goal_met, status_out, fail_flag, auto_reset, seed,
-                                          env_offset));
+                                          stream, B, x, aux, step, u_rl, episode, mu, sigma, obs_out, u_out, reward,
+                                          cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset,
+                                          *prm));
     return launch_status();
 }
 
@@ -317,8 +317,8 @@ int rcbf_safe_step_seq(const rcbf_params* prm, int64_t B, int32_t K, double* x, 
     RCBF_DISPATCH(prm, {
         for (int32_t j = 0; j < K; ++j) {
             hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0, stream,
-                               *prm, B, x, aux, step, episode, u_rl_seq[j % n_u_rl], mu, sigma, obs_out, u_out,
-                               reward, cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset);
+                               B, x, aux, step, u_rl_seq[j % n_u_rl], episode, mu, sigma, obs_out, u_out, reward,
+                               cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset, *prm);
             if (int e = launch_status()) return e;
         }
     });

@@ -14,8 +14,8 @@ extern "C" int rcbf_study_safe_step_stamps(const rcbf_params* prm, int64_t B, do
     if (int e = check_prm(prm)) return e;
     if (B <= 0 || !stamps) return RCBF_E_BAD_SHAPE;
     RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_, true>), dim3(grid_for_envs(B)), dim3(kBlock),
-                                          0, stream, *prm, B, x, aux, step, episode, u_rl, nullptr, nullptr, obs_out,
-                                          u_out, reward, cost, done, nullptr, nullptr, nullptr, auto_reset, seed,
-                                          (int64_t)0, stamps));
+                                          0, stream, B, x, aux, step, u_rl, episode, nullptr, nullptr, obs_out, u_out,
+                                          reward, cost, done, nullptr, nullptr, nullptr, auto_reset, seed, (int64_t)0,
+                                          *prm, stamps));
     return launch_status();
 }
