@@ -43,7 +43,7 @@ PRIOR_TENSOR_BYTES = {"SimulatedCars": 12, "Unicycle": 24}
 
 
 def bytes_per_step(args):
-    return BYTES_PER_STEP[args.env] + (PRIOR_TENSOR_BYTES[args.env] if args.prior == "tensor" else 0)
+    return BYTES_PER_STEP[args.env] + (PRIOR_TENSOR_BYTES[args.env] if args.prior in ("tensor", "rows") else 0)
 
 
 def parse():
@@ -64,9 +64,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--extra", action="store_true", help="also time the K-step rollout kernel and big batches")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (for PMC counter passes)")
-    ap.add_argument("--prior", default="prior", choices=["prior", "tensor"],
+    ap.add_argument("--prior", default="prior", choices=["prior", "tensor", "rows"],
                     help="prior: the DynamicsModel prior in-kernel (before any GP fit); tensor: per-env mean/sigma "
-                         "tensors read from HBM (after the GP fit)")
+                         "read from HBM (after the GP fit) in the column layout the GP writes for the step "
+                         "(rcbf_gp_predict_cols -> rcbf_safe_step_cols); rows: the same as (B, n_s) row tensors")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="CPU/gloo plumbing check of the launcher (no kernel, no measurement)")
     ap.add_argument("--launch", default="graph", choices=["graph", "seq"],
@@ -178,7 +179,8 @@ def pmc_traffic(env_name, B, hazards=3, prior="prior"):
     passes (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, gfx950
     corrections) for this exact workload, newest round first; None if absent."""
     import glob
-    short = ("cars" if env_name == "SimulatedCars" else f"unicycle{hazards}") + ("_tensorprior" if prior == "tensor" else "")
+    short = ("cars" if env_name == "SimulatedCars" else f"unicycle{hazards}") + {"prior": "", "tensor": "_tensorprior",
+                                                                                 "rows": "_rowsprior"}[prior]
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{short}_B{B}.json")),
                        reverse=True):
         try:
@@ -379,7 +381,9 @@ def main():
         "dtype": "f32 rows / f64 QP / f64 env",
         "data": ("dry run: launcher and collectives only, no kernel, not a measurement" if args.cpu_dry_run else
                  "synthetic (SURVEY 8(d) start states, u_RL ~ U[-1,1], "
-                 + ("prior mean/sigma" if args.prior == "prior" else "per-env mean/sigma tensors (post-GP-fit regime)")
+                 + {"prior": "prior mean/sigma",
+                    "tensor": "per-env mean/sigma, column layout of rcbf_gp_predict_cols (post-GP-fit regime)",
+                    "rows": "per-env mean/sigma (B, n_s) row tensors (post-GP-fit regime)"}[args.prior]
                  + ", seeded auto-resets)"),
         "config": {"workload": f"{args.env} fused safe step (rcbf_safe_step), non-diff CBF-QP, {hz}"
                                f"batch {B} envs per GPU, {args.solver} fp64 QP, {launch}",
@@ -443,16 +447,21 @@ def setup_gpu(args, dev, rank, B):
     # 50 distinct u_RL batches, cycled through by the captured steps
     pool = [(torch.rand(B, env.n_u, device=dev, generator=gen) * 2 - 1).contiguous() for _ in range(min(S, 50))]
     mean = sigma = None
-    if args.prior == "tensor":  # a fitted GP's per-env posterior (dynamics.py:342-390): small mean, sigma near MAX_STD
+    layout = "cols" if args.prior == "tensor" else "rows"
+    if args.prior in ("tensor", "rows"):  # a fitted GP's per-env posterior (dynamics.py:342-390): small mean, sigma near MAX_STD
         mean = (0.01 * torch.randn(B, env.n_s, device=dev, generator=gen)).contiguous()
         sigma = (0.2 * torch.rand(B, env.n_s, device=dev, generator=gen) + 0.05).contiguous()
+        if layout == "cols":  # what GPDisturbanceModel.predict_cols writes for the step
+            cols = list(env.PRIOR_COLS[args.env])
+            sigma = sigma[:, cols].t().contiguous()
+            mean = None if args.env == "SimulatedCars" else mean[:, cols].t().contiguous()
     outs = env.make_outputs()
     if args.env == "SimulatedCars":
         outs["goal_met"] = None
 
     def steps(n, off=0):
         for j in range(n):
-            env.safe_step(pool[(off + j) % len(pool)], layer, mean=mean, sigma=sigma, outputs=outs)
+            env.safe_step(pool[(off + j) % len(pool)], layer, mean=mean, sigma=sigma, outputs=outs, prior_layout=layout)
 
     # fraction of envs whose safety filter changes the action at the start states
     steps(1)
@@ -735,6 +744,57 @@ def next_rows(dev):
     return out
 
 
+def cascade_rows(dev):
+    """SURVEY 8(a) row a12 at config size: CascadeCBFLayer.get_u_safe
+    (rcbf_cascade_u_safe: fp64 rows, normalisation, exact QP) on 4096 cars
+    rows (config-2 start states, gamma_b 20, k_d 3) and 4096 unicycle rows
+    (k = 3 hazards, gamma_b 40, k_d 3), one launch each, hipGraph-timed; the
+    algorithmic bytes per QP are the fp64 inputs and the fp64 u_safe."""
+    import ctypes
+    from rcbf_amd import _lib
+    from rcbf_amd.cbf_qp import CascadeCBFLayer
+    from rcbf_amd.envs import SimulatedCarsEnv, UnicycleEnv
+    lib = _lib.load()
+    out = {}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(23)
+    B = 4096
+    cars = BatchedStartStates.cars(B, dev, gen)
+    uni = UnicycleEnv()
+    uni.hazards_locations = uni.hazards_locations[:3]
+    for name, layer, X, n_u, n_s in (("cars", CascadeCBFLayer(SimulatedCarsEnv(), gamma_b=20.0, k_d=3.0), cars, 1, 10),
+                                     ("unicycle3", CascadeCBFLayer(uni, gamma_b=40.0, k_d=3.0, l_p=0.03),
+                                      torch.cat([torch.rand(B, 2, device=dev, generator=gen, dtype=torch.float64) * 6 - 3,
+                                                 (torch.rand(B, 1, device=dev, generator=gen, dtype=torch.float64) * 2 - 1)
+                                                 * math.pi], 1).contiguous(), 2, 3)):
+        U = (torch.rand(B, n_u, device=dev, generator=gen, dtype=torch.float64) * 2 - 1).contiguous()
+        M = torch.zeros(B, n_s, dtype=torch.float64, device=dev)
+        S = torch.full((B, n_s), 0.2, dtype=torch.float64, device=dev)
+        if name == "cars":
+            S[:, 0::2] = 0.0
+        o = torch.empty(B, n_u, dtype=torch.float64, device=dev)
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        def launch():
+            lib.rcbf_cascade_u_safe(ctypes.byref(layer._prm), B, _lib.ptr(U), _lib.ptr(X), _lib.ptr(M), _lib.ptr(S),
+                                    _lib.ptr(o), None, _lib.ptr(flag), _lib.stream_of(dev))
+        ms = _time_graph(launch, 50, dev)
+        nbytes = B * 8 * (n_u + 3 * n_s + n_u)
+        out[f"cascade_u_safe_{name}_B{B}"] = {"us": round(ms * 1e3, 2), "qps_per_s": round(B / ms * 1e3, 1),
+                                              "GBs": round(nbytes / ms / 1e6, 1)}
+    return out
+
+
+class BatchedStartStates:
+    @staticmethod
+    def cars(B, dev, gen):
+        """Config-2 start states (bench.init_states), as an fp64 (B, 10) tensor."""
+        from rcbf_amd.envs import BatchedSimulatedCarsEnv
+        env = BatchedSimulatedCarsEnv(B, device=dev, seed=77)
+        init_states(env, gen, "SimulatedCars")
+        return env.state.double().contiguous()
+
+
 def extra_measurements(env, layer, dev, args):
     """Secondary numbers (not `value`): the K-step rollout kernel (state in
     registers across steps) and the fused step at a batch beyond the 256 MiB
@@ -754,6 +814,7 @@ def extra_measurements(env, layer, dev, args):
     out["rollout_K100_steps_per_s"] = round(env.num_envs * K / (ms * 1e-3), 1)
     out.update(sac_update_safe_action(env, layer, dev))
     out.update(generic_qp_rows(layer, dev))
+    out.update(cascade_rows(dev))
     out.update(next_rows(dev))
     if args.env == "SimulatedCars":
         Bb = 4 * 1024 * 1024

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 7
+#define RCBF_ABI_VERSION 8
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -226,6 +226,15 @@ int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B);
 int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out,
                     float* std_out, float* workspace, hipStream_t stream);
 
+/* rcbf_gp_predict that also (or only) writes the COLUMN layout the fused
+ * step reads (rcbf_safe_step_cols): mean_cols / std_cols (n_cols, B) f32 of
+ * the output dimensions cols[0..n_cols) (a host array, n_cols <= 10), e.g.
+ * cars std columns {5, 7, 9}.  mean_out / std_out (B, n_s) and the column
+ * outputs are each nullable (at least one output). */
+int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out,
+                         float* std_out, const int32_t* cols, int32_t n_cols, float* mean_cols,
+                         float* std_cols, float* workspace, hipStream_t stream);
+
 /* ---------------------------------------------------------------------- */
 /* Model-based rollouts and the device replay buffer  */
 /* ---------------------------------------------------------------------- */
@@ -333,6 +342,21 @@ int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, in
                    float* obs_out, float* u_out, float* reward, float* cost, uint8_t* done,
                    uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag,
                    int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream);
+
+/* rcbf_safe_step with the disturbance prediction in COLUMN layout: only the
+ * entries the CBF rows read, one contiguous (B,) f32 column each, as
+ * rcbf_gp_predict_cols writes them after a GP fit (dynamics.py:342-390
+ * feeding diff_cbf_qp.py:241, 261, 299).  Cars: sigma_cols (3, B) =
+ * sigma[:, 5], sigma[:, 7], sigma[:, 9]; mu_cols must be NULL (the cars rows
+ * ignore the mean).  Unicycle: mu_cols, sigma_cols (3, B).  NULL -> the
+ * prior, as in rcbf_safe_step.  Same results as rcbf_safe_step on the
+ * (B, n_s) rows holding the same values; 12 B instead of whole 40-B rows per
+ * cars env. */
+int rcbf_safe_step_cols(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step,
+                        uint32_t* episode, const float* u_rl, const float* mu_cols, const float* sigma_cols,
+                        float* obs_out, float* u_out, float* reward, float* cost, uint8_t* done,
+                        uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag, int32_t auto_reset,
+                        uint64_t seed, int64_t env_offset, hipStream_t stream);
 
 /* K fused safe steps issued back to back from one host call: K launches of
  * the same kernel as rcbf_safe_step on `stream` (each step reads and writes

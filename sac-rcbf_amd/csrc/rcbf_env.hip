@@ -285,10 +285,15 @@ int rcbf_host_alloc(int64_t bytes, void** ptr) {
 
 int rcbf_host_free(void* ptr) { return ptr ? (int)hipHostFree(ptr) : 0; }
 
-int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
-                   const float* u_rl, const float* mu, const float* sigma, float* obs_out, float* u_out,
-                   float* reward, float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
-                   int32_t* fail_flag, int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream) {
+}  // extern "C"
+
+namespace {
+
+int safe_step_launch(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
+                     const float* u_rl, const float* mu, const float* sigma, float* obs_out, float* u_out,
+                     float* reward, float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
+                     int32_t* fail_flag, int32_t auto_reset, uint64_t seed, int64_t env_offset, int cols,
+                     hipStream_t stream) {
     if (int e = check_prm(prm)) return e;
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
@@ -297,8 +302,30 @@ int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, in
     RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0,
                                           stream, B, x, aux, step, u_rl, episode, mu, sigma, obs_out, u_out, reward,
                                           cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset,
-                                          *prm));
+                                          *prm, cols));
     return launch_status();
+}
+
+}  // namespace
+
+extern "C" {
+
+int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
+                   const float* u_rl, const float* mu, const float* sigma, float* obs_out, float* u_out,
+                   float* reward, float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
+                   int32_t* fail_flag, int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream) {
+    return safe_step_launch(prm, B, x, aux, step, episode, u_rl, mu, sigma, obs_out, u_out, reward, cost, done,
+                            goal_met, status_out, fail_flag, auto_reset, seed, env_offset, 0, stream);
+}
+
+int rcbf_safe_step_cols(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
+                        const float* u_rl, const float* mu_cols, const float* sigma_cols, float* obs_out,
+                        float* u_out, float* reward, float* cost, uint8_t* done, uint8_t* goal_met,
+                        int32_t* status_out, int32_t* fail_flag, int32_t auto_reset, uint64_t seed,
+                        int64_t env_offset, hipStream_t stream) {
+    if (prm && prm->mode == RCBF_MODE_SIMULATED_CARS && mu_cols) return RCBF_E_BAD_SHAPE;  // the cars rows read no mean
+    return safe_step_launch(prm, B, x, aux, step, episode, u_rl, mu_cols, sigma_cols, obs_out, u_out, reward, cost,
+                            done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset, 1, stream);
 }
 
 int rcbf_safe_step_seq(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux, int32_t* step,
@@ -318,7 +345,7 @@ int rcbf_safe_step_seq(const rcbf_params* prm, int64_t B, int32_t K, double* x, 
         for (int32_t j = 0; j < K; ++j) {
             hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0, stream,
                                B, x, aux, step, u_rl_seq[j % n_u_rl], episode, mu, sigma, obs_out, u_out, reward,
-                               cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset, *prm);
+                               cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset, *prm, 0);
             if (int e = launch_status()) return e;
         }
     });

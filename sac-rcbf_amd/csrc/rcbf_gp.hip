@@ -328,10 +328,17 @@ __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, 
 }
 
 // mean/std (B, n_s) row-major like predict_disturbance's (n_test, n_s) output.
+// The output dimensions written in column layout (rcbf_gp_predict_cols).
+struct GpCols {
+    int32_t n;
+    int32_t idx[10];
+};
+
 __global__ void __launch_bounds__(256) k_gp_finish(rcbf_gp_model m, int64_t B, int n_cb,
                                                    const float* __restrict__ partial,
                                                    const float* __restrict__ meanraw, float* __restrict__ mean_out,
-                                                   float* __restrict__ std_out) {
+                                                   float* __restrict__ std_out, GpCols cols,
+                                                   float* __restrict__ mean_cols, float* __restrict__ std_cols) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= B * m.n_s) return;
     const int i = (int)(e % m.n_s);
@@ -340,8 +347,15 @@ __global__ void __launch_bounds__(256) k_gp_finish(rcbf_gp_model m, int64_t B, i
     for (int c = 0; c < n_cb; ++c) q += partial[((int64_t)i * n_cb + c) * B + b];
     const float lat = fmaxf(m.outscale[i] - q, 0.0f);  // latent posterior variance
     const float var = lat + m.noise[i];                  // likelihood(model(x)).variance
-    mean_out[e] = meanraw[(int64_t)i * B + b] * m.y_scale[i];
-    std_out[e] = sqrtf(var) * m.y_scale[i];
+    const float mu = meanraw[(int64_t)i * B + b] * m.y_scale[i];
+    const float sd = sqrtf(var) * m.y_scale[i];
+    if (mean_out) mean_out[e] = mu;
+    if (std_out) std_out[e] = sd;
+    for (int c = 0; c < cols.n; ++c) {
+        if (cols.idx[c] != i) continue;
+        if (mean_cols) mean_cols[(int64_t)c * B + b] = mu;
+        if (std_cols) std_cols[(int64_t)c * B + b] = sd;
+    }
 }
 
 // Split-K factor: 1 when the (query tile x column block x GP) grid already
@@ -380,12 +394,27 @@ int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B) {
 
 int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out, float* std_out,
                     float* workspace, hipStream_t stream) {
+    if (!mean_out || !std_out) return RCBF_E_NULL;
+    return rcbf_gp_predict_cols(m, B, x, mean_out, std_out, nullptr, 0, nullptr, nullptr, workspace, stream);
+}
+
+int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out, float* std_out,
+                         const int32_t* cols, int32_t n_cols, float* mean_cols, float* std_cols, float* workspace,
+                         hipStream_t stream) {
     if (!m) return RCBF_E_NULL;
+    GpCols gc{};
+    if (n_cols < 0 || n_cols > 10 || (n_cols > 0 && !cols)) return RCBF_E_BAD_SHAPE;
+    gc.n = (mean_cols || std_cols) ? n_cols : 0;
+    for (int c = 0; c < gc.n; ++c) {
+        if (cols[c] < 0 || cols[c] >= m->n_s) return RCBF_E_BAD_SHAPE;
+        gc.idx[c] = cols[c];
+    }
+    if (!mean_out && !std_out && gc.n == 0) return RCBF_E_NULL;  // nothing to write
     if (B < 0 || m->n_s < 1 || m->n_s > 10 || m->N < 1 || m->N_pad % 32 || m->N_pad < m->N || m->r < 1 ||
         m->r > m->N || m->C_pad % kGpCols || m->C_pad < m->r + 1)
         return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
-    if (!x || !mean_out || !std_out || !workspace || !m->xt || !m->tn2 || !m->Rt || !m->x_std || !m->inv_sl ||
+    if (!x || !workspace || !m->xt || !m->tn2 || !m->Rt || !m->x_std || !m->inv_sl ||
         !m->outscale || !m->noise || !m->y_scale)
         return RCBF_E_NULL;
     const int n_cb = m->C_pad / kGpCols;
@@ -452,7 +481,7 @@ int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* me
     }
     const int64_t tot = B * m->n_s;
     hipLaunchKernelGGL(k_gp_finish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *m, B, n_part,
-                       partial, meanraw, mean_out, std_out);
+                       partial, meanraw, mean_out, std_out, gc, mean_cols, std_cols);
     return launch_status();
 }
 

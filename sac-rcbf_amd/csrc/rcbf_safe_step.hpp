@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
                                                       uint8_t* __restrict__ goal_met,
                                                       int32_t* __restrict__ status_out, int32_t* fail_flag,
                                                       int auto_reset, uint64_t seed, int64_t off, rcbf_params prm,
-                                                      unsigned long long* stamp_buf = nullptr) {
+                                                      int prior_cols = 0, unsigned long long* stamp_buf = nullptr) {
     using D = Dims<MODE, K>;
     int64_t i = env_index();
     if (i >= B) return;
@@ -165,10 +165,35 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
     const bool ep_pre = episode && reset_foreseeable<MODE>(st, a);
     uint32_t ep0 = 0;
     if (ep_pre) ep0 = episode[i];
+    if (prior_cols) {
+        // column layout (rcbf_safe_step_cols): only what the rows read, one
+        // contiguous (B,) f32 column each -- cars sigma (3, B) = sigma[:, 5],
+        // [:, 7], [:, 9] (the cars rows ignore mu, diff_cbf_qp.py:298-299);
+        // unicycle mu and sigma (3, B)
 #pragma unroll
-    for (int k = 0; k < D::NS; ++k) {
-        m[k] = mu ? mu[i * D::NS + k] : 0.0f;
-        s[k] = sigma ? sigma[i * D::NS + k] : prior_sigma<MODE>(k);
+        for (int k = 0; k < D::NS; ++k) {
+            m[k] = 0.0f;
+            s[k] = prior_sigma<MODE>(k);
+        }
+        if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
+            if (sigma) {
+                s[5] = ld_in(&sigma[i]);
+                s[7] = ld_in(&sigma[B + i]);
+                s[9] = ld_in(&sigma[2 * B + i]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < D::NS; ++k) {
+                if (mu) m[k] = ld_in(&mu[k * B + i]);
+                if (sigma) s[k] = ld_in(&sigma[k * B + i]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < D::NS; ++k) {
+            m[k] = mu ? mu[i * D::NS + k] : 0.0f;
+            s[k] = sigma ? sigma[i * D::NS + k] : prior_sigma<MODE>(k);
+        }
     }
     float rew, cst;
     bool dn, gm;

@@ -16,6 +16,6 @@ extern "C" int rcbf_study_safe_step_stamps(const rcbf_params* prm, int64_t B, do
     RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_, true>), dim3(grid_for_envs(B)), dim3(kBlock),
                                           0, stream, B, x, aux, step, u_rl, episode, nullptr, nullptr, obs_out, u_out,
                                           reward, cost, done, nullptr, nullptr, nullptr, auto_reset, seed, (int64_t)0,
-                                          *prm, stamps));
+                                          *prm, 0, stamps));
     return launch_status();
 }

@@ -23,7 +23,7 @@ SOLVER_PDIPM = 1
 SOLVER_GI = 2
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NONFINITE = 0, 1, 2, 3
 MAX_HAZARDS = 8
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL"}
 
@@ -85,11 +85,14 @@ SIGNATURES = {
     "rcbf_ring_scatter_f64": [_P, _I64, _I64, _I64, _P, _I64, _P],
     "rcbf_gather_rows_f64": [_P, _P, _I64, _P, _I64, _P],
     "rcbf_gp_predict": [_GPM, _I64, _P, _P, _P, _P, _P],
+    "rcbf_gp_predict_cols": [_GPM, _I64, _P, _P, _P, _P, _I32, _P, _P, _P, _P],
     "rcbf_obs_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_cascade_u_safe": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_env_reset": [_PRM, _I64, _P, _P, _U64, _I64, _P, _P, _P, _P, _P, _P],
     "rcbf_env_step": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
     "rcbf_safe_step": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
+    "rcbf_safe_step_cols": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64,
+                            _P],
     "rcbf_safe_rollout": [_PRM, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _P],
     "rcbf_safe_step_seq": [_PRM, _I64, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                            _I32, _U64, _I64, _P],

@@ -226,7 +226,24 @@ class BatchedEnv:
             raise ValueError(f"{name} must be ({B}, {self.n_s}), got {tuple(t.shape)}")
         return t
 
-    def safe_step(self, u_rl, layer, mean=None, sigma=None, auto_reset=True, outputs=None):
+    # output dimensions of the disturbance prediction the CBF rows read, in
+    # the column layout of rcbf_safe_step_cols: cars sigma[:, 5], [:, 7],
+    # [:, 9] (no mean, diff_cbf_qp.py:298-299); unicycle all three of each
+    PRIOR_COLS = {"SimulatedCars": (5, 7, 9), "Unicycle": (0, 1, 2)}
+
+    def _prior_cols_arg(self, t, name):
+        """mean / sigma in column layout: (len(PRIOR_COLS), B) fp32."""
+        if t is None:
+            return None
+        B, d = self.num_envs, self.device
+        if not (torch.is_tensor(t) and t.dtype == torch.float32 and t.is_contiguous() and t.device == d):
+            t = torch.as_tensor(t, dtype=torch.float32, device=d).contiguous()
+        nc = len(self.PRIOR_COLS[self.dynamics_mode])
+        if t.shape != (nc, B):
+            raise ValueError(f"{name} (column layout) must be ({nc}, {B}), got {tuple(t.shape)}")
+        return t
+
+    def safe_step(self, u_rl, layer, mean=None, sigma=None, auto_reset=True, outputs=None, prior_layout="rows"):
         """The fused hot path (rcbf_safe_step): state -> get_state(obs32) ->
         CBFQPLayer.get_safe_action(state, u_rl, mean, sigma) -> env.step.
         mean/sigma None -> the DynamicsModel prior in-kernel.  `outputs`
@@ -237,6 +254,21 @@ class BatchedEnv:
         input, so the host keeps pace with the ~4 us kernel."""
         o = outputs if outputs is not None else self.make_outputs()
         u = self._u_arg(u_rl)
+        if prior_layout == "cols":
+            # (len(PRIOR_COLS), B) columns (rcbf_safe_step_cols; e.g. GPDisturbanceModel.predict_cols)
+            if mean is not None and self.dynamics_mode == "SimulatedCars":
+                raise ValueError("the cars CBF rows read no mean (diff_cbf_qp.py:298-299): pass mean=None")
+            mean, sigma = self._prior_cols_arg(mean, "mean"), self._prior_cols_arg(sigma, "sigma")
+            args = self._step_args(layer, o, auto_reset)
+            rc = _lib.load().rcbf_safe_step_cols(
+                ctypes.byref(layer._prm), self.num_envs, *[a or None for a in args[2:6]], u.data_ptr(),
+                None if mean is None else mean.data_ptr(), None if sigma is None else sigma.data_ptr(),
+                *[a or None for a in args[9:17]], *args[17:20],
+                torch._C._cuda_getCurrentRawStream(self.device.index) or None)
+            _lib.check(rc, "rcbf_safe_step_cols")
+            return self.obs, o["reward"], o["done"], o
+        if prior_layout != "rows":
+            raise ValueError(f"prior_layout must be 'rows' or 'cols', got {prior_layout!r}")
         mean, sigma = self._prior_arg(mean, "mean"), self._prior_arg(sigma, "sigma")
         args = self._step_args(layer, o, auto_reset)
         args[6] = u.data_ptr()

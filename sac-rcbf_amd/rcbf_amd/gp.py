@@ -144,6 +144,30 @@ class GPDisturbanceModel:
         _lib.check(rc, "rcbf_gp_predict")
         return mean, std
 
+    def predict_cols(self, x, cols, mean=True, rows=False):
+        """The same posterior in the COLUMN layout the fused step reads
+        (rcbf_gp_predict_cols -> rcbf_safe_step_cols): (mean_cols, std_cols),
+        each (len(cols), B) float32 (mean_cols None when mean=False, e.g. the
+        cars std columns (5, 7, 9), whose rows ignore the mean); with rows=True
+        also the (B, n_s) rows: (mean_cols, std_cols, mean, std)."""
+        lib = _lib.load()
+        x = x.to(device=self.device, dtype=torch.float32).contiguous()
+        B = x.shape[0]
+        cols = [int(c) for c in cols]
+        carr = (ctypes.c_int32 * max(1, len(cols)))(*cols)
+        mc = torch.empty(len(cols), B, dtype=torch.float32, device=self.device) if mean else None
+        sc = torch.empty(len(cols), B, dtype=torch.float32, device=self.device)
+        mr = torch.empty(B, self.n_s, dtype=torch.float32, device=self.device) if rows else None
+        sr = torch.empty_like(mr) if rows else None
+        need = int(lib.rcbf_gp_workspace_floats(ctypes.byref(self._m), B))
+        if self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
+        rc = lib.rcbf_gp_predict_cols(ctypes.byref(self._m), B, _lib.ptr(x), _lib.ptr(mr), _lib.ptr(sr), carr,
+                                      len(cols), _lib.ptr(mc), _lib.ptr(sc), _lib.ptr(self._ws),
+                                      _lib.stream_of(self.device))
+        _lib.check(rc, "rcbf_gp_predict_cols")
+        return (mc, sc, mr, sr) if rows else (mc, sc)
+
     def flops_per_query(self):
         """Algorithmic MFMA flops per query row: 2 N C_pad per GP."""
         return 2 * self.N * self._m.C_pad * self.n_s

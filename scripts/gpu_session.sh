@@ -29,19 +29,20 @@ wl_args() {  # bench.py arguments of a workload
     uni3) echo "--env Unicycle --hazards 3" ;;
     uni5) echo "--env Unicycle --hazards 5" ;;
     carsT) echo "--env SimulatedCars --prior tensor" ;;
+    carsR) echo "--env SimulatedCars --prior rows" ;;
     uni5T) echo "--env Unicycle --hazards 5 --prior tensor" ;;
   esac
 }
 wl_kernel() {  # the fused kernel's name in rocprofv3 output
   case $1 in
-    cars|carsT) echo 'k_safe_step<0, 0, 1, false>' ;;
+    cars|carsT|carsR) echo 'k_safe_step<0, 0, 1, false>' ;;
     uni3) echo 'k_safe_step<0, 1, 3, false>' ;;
     uni5|uni5T) echo 'k_safe_step<0, 1, 5, false>' ;;
   esac
 }
 wl_name() {
   case $1 in cars) echo cars ;; uni3) echo unicycle3 ;; uni5) echo unicycle5 ;;
-    carsT) echo cars_tensorprior ;; uni5T) echo unicycle5_tensorprior ;; esac
+    carsT) echo cars_tensorprior ;; carsR) echo cars_rowsprior ;; uni5T) echo unicycle5_tensorprior ;; esac
 }
 for step in "$@"; do
   wl=${step#*_}

@@ -14,7 +14,8 @@ STUDY_LIB = os.path.join(ROOT, "build", "study", "librcbf_stamps.so")
 if "--build" in sys.argv:
     os.makedirs(os.path.dirname(STUDY_LIB), exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-fhip-fp32-correctly-rounded-divide-sqrt", "-I" + os.path.join(ROOT, "include"),
+           "-fhip-fp32-correctly-rounded-divide-sqrt", "-mllvm", "-amdgpu-kernarg-preload-count=16",
+           "-I" + os.path.join(ROOT, "include"),
            "-I" + os.path.join(ROOT, "sac-rcbf_amd", "csrc"), "-o", STUDY_LIB,
            os.path.join(ROOT, "sac-rcbf_amd", "csrc", "study", "rcbf_stamps.hip")]
     subprocess.run(cmd, check=True)

@@ -441,6 +441,42 @@ def make_cascade(SimulatedCarsEnv, UnicycleEnv, cbf_qp, B=256, seed=5):
     return out
 
 
+def make_cascade_config(SimulatedCarsEnv, UnicycleEnv, cbf_qp, B=4096, seed=23):
+    """Cascade rows at config size (SURVEY 8(c)(ii) per config): cars B = 4096
+    from the config-2 start-state distribution (gamma_b = 20, k_d = 3,
+    simulated_cars_env.py:170-171) and unicycle with the config-3 hazard set
+    (the first 3 hazards, gamma_b = 40, k_d = 3, unicycle_env.py:334-340),
+    through the reference's own CascadeCBFLayer.get_u_safe with the exact QP
+    in place of quadprog (cbf_qp.py:276)."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    env = SimulatedCarsEnv()
+    layer = cbf_qp.CascadeCBFLayer(env, gamma_b=20.0, k_d=3.0)
+    states, _ = _rollout_cars_states(SimulatedCarsEnv, B, rng)
+    un = rng.uniform(-1, 1, (B, 1))
+    mu = np.zeros((B, 10))
+    sig = np.tile(np.array([0, .2, 0, .2, 0, .2, 0, .2, 0, .2]), (B, 1))
+    us = []
+    for i in range(B):
+        with contextlib.redirect_stdout(io.StringIO()):
+            us.append(layer.get_u_safe(un[i], states[i], mu[i], sig[i]))
+    out.update(cars_x=states, cars_u=un, cars_mu=mu, cars_sigma=sig, cars_usafe=np.array(us))
+    env = UnicycleEnv()
+    env.hazards_locations = env.hazards_locations[:3]
+    layer = cbf_qp.CascadeCBFLayer(env, gamma_b=40.0, k_d=3.0, l_p=0.03)
+    xs = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+    un = rng.uniform(-1, 1, (B, 2))
+    mu = rng.normal(0, 0.1, (B, 3))
+    sig = rng.uniform(0, 0.3, (B, 3))
+    us = []
+    for i in range(B):
+        with contextlib.redirect_stdout(io.StringIO()):
+            us.append(layer.get_u_safe(un[i], xs[i], mu[i], sig[i]))
+    out.update(uni3_x=xs, uni3_u=un, uni3_mu=mu, uni3_sigma=sig, uni3_usafe=np.array(us),
+               uni3_hazards=np.asarray(env.hazards_locations, np.float64))
+    return out
+
+
 def make_env_traj(SimulatedCarsEnv, UnicycleEnv, seed=7):
     rng = np.random.default_rng(seed)
     out = {}
@@ -645,6 +681,7 @@ def main():
         "unicycle3_layer.npz": lambda: make_unicycle_layer(UnicycleEnv, diff_cbf_qp, 3),
         "unicycle5_layer.npz": lambda: make_unicycle_layer(UnicycleEnv, diff_cbf_qp, 5),
         "cascade.npz": lambda: make_cascade(SimulatedCarsEnv, UnicycleEnv, cbf_qp),
+        "cascade_config.npz": lambda: make_cascade_config(SimulatedCarsEnv, UnicycleEnv, cbf_qp),
         "env_traj.npz": lambda: make_env_traj(SimulatedCarsEnv, UnicycleEnv),
         "closed_loop_cars.npz": lambda: make_closed_loop(SimulatedCarsEnv, cbf_qp, dynamics),
         "dynamics.npz": lambda: make_dynamics(SimulatedCarsEnv, UnicycleEnv, dynamics),

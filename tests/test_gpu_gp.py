@@ -148,3 +148,47 @@ def test_gp_predict_low_rank_split_k():
     mean, std = model.predict(torch.as_tensor(q, device="cuda"))
     mo, so = O.gp_predict(q, tx, ty, hyper, rank=100)
     _check(mean.cpu().numpy(), std.cpu().numpy(), mo, so)
+
+
+@pytest.mark.parametrize("n_s,cols,B", [(10, (5, 7, 9), 4096), (10, (5, 7, 9), 3), (3, (0, 1, 2), 1000)])
+def test_gp_predict_cols_equals_rows(n_s, cols, B):
+    """rcbf_gp_predict_cols writes, in the column layout the fused step reads
+    (rcbf_safe_step_cols), exactly the values rcbf_gp_predict writes as rows;
+    the rows outputs are optional; and a fused step fed the columns equals one
+    fed the rows, bit for bit."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(B + n_s)
+    tx, ty = _data(rng, 600, n_s)
+    model = gp.GPDisturbanceModel(tx, ty, [(1.3, 0.2, 0.05)] * n_s)
+    q = torch.as_tensor((rng.normal(0, 1, (B, n_s)) * tx.std(0)).astype(np.float32), device="cuda")
+    mean, std = model.predict(q)
+    mc, sc, mr, sr = model.predict_cols(q, cols, rows=True)
+    assert torch.equal(mr, mean) and torch.equal(sr, std)
+    assert torch.equal(sc, std[:, list(cols)].t()) and torch.equal(mc, mean[:, list(cols)].t())
+    mc2, sc2 = model.predict_cols(q, cols, mean=False)
+    assert mc2 is None and torch.equal(sc2, sc)
+    if B < 64:
+        return
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+
+    class A:
+        cuda = True
+    runs = []
+    for layout in ("rows", "cols"):
+        if n_s == 10:
+            env = BatchedSimulatedCarsEnv(B, seed=3)
+        else:
+            env = BatchedUnicycleEnv(B, seed=3, hazards_locations=O.UNI["hazards"][:3])
+            env.load_state(np.stack([rng.uniform(-3, 3, B) * 0 + np.linspace(-3, 3, B), np.linspace(3, -3, B),
+                                     np.linspace(-3, 3, B)], 1), np.ones(B), np.zeros(B))
+        lay = CBFQPLayer(env, A(), gamma_b=20.0)
+        u = torch.linspace(-1, 1, B * env.n_u, device="cuda").reshape(B, env.n_u).contiguous()
+        if layout == "rows":
+            obs, r, d, o = env.safe_step(u, lay, mean=mean, sigma=std)
+        else:
+            obs, r, d, o = env.safe_step(u, lay, mean=None if n_s == 10 else mc, sigma=sc, prior_layout="cols")
+        env.check_failures()
+        runs.append([obs.clone(), r.clone(), o["u"].clone(), env.state.clone()])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)

@@ -82,10 +82,15 @@ def run_teacher_forced(mode, B, steps, hazards=3, pool=8, prior="prior"):
     bench.init_states(env, gen, mode)
     us = [(torch.rand(B, env.n_u, device=env.device, generator=gen) * 2 - 1).contiguous() for _ in range(pool)]
     mean = sigma = mean_h = sigma_h = None
-    if prior == "tensor":  # bench.setup_gpu's post-GP-fit stand-in: small mean, sigma near MAX_STD
+    layout = "rows"
+    if prior in ("tensor", "cols"):  # bench.setup_gpu's post-GP-fit stand-in: small mean, sigma near MAX_STD
         mean = (0.01 * torch.randn(B, env.n_s, device=env.device, generator=gen)).contiguous()
         sigma = (0.2 * torch.rand(B, env.n_s, device=env.device, generator=gen) + 0.05).contiguous()
         mean_h, sigma_h = mean.cpu().numpy(), sigma.cpu().numpy()
+        if prior == "cols":  # the device reads the column layout of rcbf_safe_step_cols, the oracle the rows
+            layout, cols = "cols", list(env.PRIOR_COLS[mode])
+            sigma = sigma[:, cols].t().contiguous()
+            mean = None if mode == "SimulatedCars" else mean[:, cols].t().contiguous()
     outs = env.make_outputs()
     hz = env.hazards_locations if mode == "Unicycle" else None
     idx = env.env_offset + np.arange(B)
@@ -93,7 +98,7 @@ def run_teacher_forced(mode, B, steps, hazards=3, pool=8, prior="prior"):
     for k in range(steps):
         x, aux, st, ep = _snapshot(env)
         u = us[k % pool]
-        env.safe_step(u, layer, mean=mean, sigma=sigma, outputs=outs)
+        env.safe_step(u, layer, mean=mean, sigma=sigma, outputs=outs, prior_layout=layout)
         torch.cuda.synchronize()
         u_h = u.cpu().numpy()
         noise = 0.5 * O.normal_draw(env._rng_seed(), idx, ep + 1) if mode == "SimulatedCars" else None
@@ -161,6 +166,17 @@ def test_headline_unicycle_B65536_tensor_prior_vs_oracle(k):
     """The post-GP-fit regime for the unicycle: per-env mu and sigma enter
     the hazard rows (diff_cbf_qp.py:241, 261)."""
     r = run_teacher_forced("Unicycle", 65536, 24, hazards=k, prior="tensor")
+    assert r["resets"] > 500
+    assert r["filter_active"] > 0.02 * r["env_steps"]
+
+
+@pytest.mark.parametrize("mode,k", [("SimulatedCars", 3), ("Unicycle", 5)])
+def test_headline_tensor_prior_column_layout_vs_oracle(mode, k):
+    """The post-GP-fit regime as bench.py --prior tensor runs it: the
+    disturbance prediction in the column layout rcbf_gp_predict_cols writes
+    (cars sigma[:, 5/7/9], unicycle mean and sigma), read by
+    rcbf_safe_step_cols; the oracle gets the same values as (B, n_s) rows."""
+    r = run_teacher_forced(mode, 65536, 24, hazards=k, prior="cols")
     assert r["resets"] > 500
     assert r["filter_active"] > 0.02 * r["env_steps"]
 

@@ -180,6 +180,24 @@ def test_cascade_golden(golden):
     assert one.shape == (2,) and rel(one, c["uni_usafe"][0]) <= 1e-7
 
 
+def test_cascade_config_size_golden(golden):
+    """rcbf_cascade_u_safe at config size: 4096 cars rows (config-2 start
+    states) and 4096 unicycle rows with the config-3 hazard set (k = 3),
+    against the reference's own CascadeCBFLayer.get_u_safe (cbf_qp.py:29-53)
+    with the exact QP at cbf_qp.py:276."""
+    from rcbf_amd.cbf_qp import CascadeCBFLayer
+    from rcbf_amd.envs import SimulatedCarsEnv, UnicycleEnv
+    c = golden("cascade_config")
+    cl = CascadeCBFLayer(SimulatedCarsEnv(), gamma_b=20.0, k_d=3.0)
+    us = cl.get_u_safe(c["cars_u"], c["cars_x"], c["cars_mu"], c["cars_sigma"])
+    assert us.shape == (4096, 1) and rel(us, c["cars_usafe"]) <= 1e-9
+    env = UnicycleEnv()
+    env.hazards_locations = np.asarray(c["uni3_hazards"])
+    ul = CascadeCBFLayer(env, gamma_b=40.0, k_d=3.0, l_p=0.03)
+    us = ul.get_u_safe(c["uni3_u"], c["uni3_x"], c["uni3_mu"], c["uni3_sigma"])
+    assert us.shape == (4096, 2) and rel(us, c["uni3_usafe"]) <= 1e-7
+
+
 def test_cascade_solve_qp_golden(golden):
     """CascadeCBFLayer.solve_qp (cbf_qp.py:242-286) on the reference's own
     rows: the exact fp64 solution (quadprog's), the caller's G normalised in

@@ -69,6 +69,21 @@ def test_cascade(golden):
     assert (st == 0).all() and rel(z[:, :2], c["uni_usafe"]) < 1e-8
 
 
+def test_cascade_config_size(golden):
+    """The Cascade layer at config size (4096 rows each): cars from the
+    config-2 start states, unicycle with the config-3 hazard set (k = 3)."""
+    c = golden("cascade_config")
+    P, G, h = O.cars_build_cascade(c["cars_x"], c["cars_u"], 20.0)
+    Gn, hn, _ = O.normalize_rows(G, h)
+    z, lam, act, st = O.qp_exact(np.diag(P), Gn, hn)
+    assert (st == 0).all() and rel(z[:, :1], c["cars_usafe"]) < 1e-9
+    P, G, h = O.unicycle_build_cascade(c["uni3_x"], c["uni3_u"], c["uni3_mu"], c["uni3_sigma"], 40.0, 3.0,
+                                       c["uni3_hazards"])
+    Gn, hn, _ = O.normalize_rows(G, h)
+    z, lam, act, st = O.qp_exact(np.diag(P), Gn, hn)
+    assert (st == 0).all() and rel(z[:, :2], c["uni3_usafe"]) < 1e-8
+
+
 def test_cars_env_traj(golden):
     d = golden("env_traj")
     for e in range(d["cars_noise"].shape[0]):
