@@ -879,6 +879,11 @@ int rcbf_qp_backward_saved(const rcbf_params* prm, int64_t B, int32_t n, int32_t
     if (B < 0 || n < 1 || n > 3 || m < 1 || m > 16) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!P || !G || !h || !grad_z) return RCBF_E_NULL;
+    // A PDIPM forward's saved point is an interior-point iterate (polished, but
+    // not certified to the active-set tightness the one-factorisation backward
+    // tests rows with): it could accept an incomplete active set, so that
+    // backward re-solves exactly instead of starting from it.
+    if (prm->solver == RCBF_SOLVER_PDIPM) z64_saved = nullptr;
     dim3 g((unsigned)((B + kQPBlock - 1) / kQPBlock)), b(kQPBlock);
     const size_t lds = (size_t)qp_lds_words(n, m) * sizeof(float);
 #define RCBF_QPB_L(NN, MP)                                                                                       \

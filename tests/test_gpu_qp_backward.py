@@ -108,6 +108,36 @@ def test_solve_qp_and_cbf_layer_autograd(normalize):
     assert rel(out.detach().cpu().numpy()[ok], want["z"][ok][:, :out.shape[1]]) <= 1e-6
 
 
+@pytest.mark.parametrize("normalize", [False, True])
+def test_solve_qp_autograd_with_pdipm_layer(normalize):
+    """The same surface with the qpth-style interior point as the forward
+    solver (solver=PDIPM): the forward's saved point is not used as an exact
+    active-set certificate (rcbf_qp_backward_saved re-solves), so gradients
+    still equal the exact implicit-KKT derivative of the oracle."""
+    from rcbf_amd import _lib
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv
+    rng = np.random.default_rng(31 + normalize)
+    B, n, m = 512, 3, 7
+    P, q, G, h = random_qps(rng, B, n, m)
+    w = rng.normal(0, 1, (B, n)).astype(np.float32)
+    layer = CBFQPLayer(BatchedSimulatedCarsEnv(4), Args(), gamma_b=20.0, solver=_lib.SOLVER_PDIPM)
+    Pt, qt, Gt, ht = (dev(a).requires_grad_(True) for a in (P, q, G, h))
+    if normalize:
+        out = layer.solve_qp(Pt, qt, Gt, ht)
+        (out * dev(w[:, :n - 1])).sum().backward()
+        w = np.concatenate([w[:, :n - 1], np.zeros((B, 1), np.float32)], axis=1)
+    else:
+        out = layer.cbf_layer(Pt, qt, Gt, ht)
+        (out * dev(w)).sum().backward()
+    want = O.qp_backward(P, q, G, h, normalize, w)
+    ok = _non_degenerate(P, q, G, h, normalize)
+    assert ok.mean() > 0.9
+    for k, t in (("P", Pt), ("q", qt), ("G", Gt), ("h", ht)):
+        assert rel(t.grad.cpu().numpy()[ok], want[k][ok]) <= 1e-5, k
+    assert rel(out.detach().cpu().numpy()[ok], want["z"][ok][:, :out.shape[1]]) <= 1e-5
+
+
 @pytest.mark.parametrize("fixture,mode", [("cars_layer", "SimulatedCars"), ("unicycle3_layer", "Unicycle"),
                                           ("unicycle5_layer", "Unicycle")])
 def test_solve_qp_grad_composes_to_reference_grad(golden, fixture, mode):
