@@ -52,6 +52,10 @@ for step in "$@"; do
     bench)  run bench 600 python bench.py ;;
     driver) run driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     benchx) run benchx 600 python bench.py --extra --no-cpu-baseline ;;
+    sweep)  # waves per SIMD: B = 32768 (half the SIMDs), 65536 (one wave each), 98304, 131072 (two)
+      for w in cars uni3 uni5; do for b in 32768 65536 98304 131072; do
+        run "sweep_${w}_$b" 300 python bench.py --no-cpu-baseline --batch "$b" $(wl_args "$w")
+      done; done ;;
     b_*)    run "b_$wl" 300 python bench.py --no-cpu-baseline $(wl_args "$wl") ;;
     prof_*)
       run "prof_$wl" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$wl" -o run -- \
