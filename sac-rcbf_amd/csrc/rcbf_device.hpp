@@ -23,6 +23,40 @@ namespace rcbf {
 
 constexpr double kInf = __builtin_huge_val();
 
+// 1: the unicycle QP's live-row test in fp32 with a conservative margin
+// (uni_qp_2d_core); 0: in fp64
+#ifndef RCBF_MASK32
+#define RCBF_MASK32 0
+#endif
+#ifndef RCBF_STUDY_NO_EDGE2
+#define RCBF_STUDY_NO_EDGE2 0
+#endif
+
+// Study build only (csrc/study/rcbf_stamps.hip defines RCBF_STUDY_QP_STAMPS
+// and the buffer): a 16-word record per wave of the unicycle QP -- s_memtime
+// at its stage boundaries (slots 0-4) and lane counts (slots 5-8), for
+// scripts/stamps.py.  Compiles to nothing in the product.
+#ifdef RCBF_STUDY_QP_STAMPS
+__device__ __forceinline__ void qp_stamp(int j) {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if ((threadIdx.x & 63) == 0 && rcbf_qp_stamp_buf)
+        rcbf_qp_stamp_buf[((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + j] = t;
+}
+__device__ __forceinline__ void qp_count(int j, bool f) {
+    const unsigned long long n = __popcll(__ballot(f));
+    if ((threadIdx.x & 63) == 0 && rcbf_qp_stamp_buf)
+        rcbf_qp_stamp_buf[((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + j] = n;
+}
+#define RCBF_QP_STAMP(j) ::rcbf::qp_stamp(j)
+#define RCBF_QP_COUNT(j, f) ::rcbf::qp_count(j, f)
+#else
+#define RCBF_QP_STAMP(j) ((void)0)
+#define RCBF_QP_COUNT(j, f) ((void)0)
+#endif
+
 // fp64 reciprocal: v_rcp_f64 + two Newton steps (error ~1 ulp), no
 // div_scale/div_fixup chain.  rcp64(0) = inf.
 // 1/d to ~11 ulp (one Newton step on v_rcp_f64, which alone is ~2^-24
@@ -1296,6 +1330,7 @@ __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2
                 }
         }
     };
+    RCBF_QP_STAMP(1);
     bu0 = 0.0;
     bu1 = 0.0;
     bool all_neg = true;
@@ -1320,6 +1355,8 @@ __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2
         bf = t ? fv : bf;
         open = open && !cert;
     }
+    RCBF_QP_STAMP(2);
+    RCBF_QP_COUNT(5, open);
     // stage 1b: kinks and triple points, for the uncertified lanes
     if (KK > 1 && __ballot(open) != 0) {
 #pragma unroll
@@ -1356,10 +1393,16 @@ __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2
     }
     const bool need0 = !((bu0 >= L0) && (bu0 <= U0)), need1 = !((bu1 >= L1) && (bu1 <= U1));
     const bool inbox = !need0 && !need1;
+    RCBF_QP_STAMP(3);
+    RCBF_QP_COUNT(6, need0);
+    RCBF_QP_COUNT(7, need1);
     // stage 2: the facing u0-edge (u0 fixed, where u_f0 leaves [L0, U0]) and
     // u1-edge (where u_f1 leaves [L1, U1]), each only in waves with such a lane
     const double v0 = fmin(fmax(bu0, L0), U0), v1 = fmin(fmax(bu1, L1), U1);
     bf = inbox ? bf : __builtin_huge_val();  // an out-of-box stage-1 point must not win
+#if RCBF_STUDY_NO_EDGE2  // timing ablation only: wrong results
+    return;
+#endif
     if (__ballot(need0) != 0) {
         double ey, ef;
         edge_solve(true, v0, L1, U1, need0, ey, ef);
@@ -1368,6 +1411,7 @@ __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2
         bu1 = t ? ey : bu1;
         bf = t ? ef : bf;
     }
+    RCBF_QP_STAMP(4);
     if (__ballot(need1) != 0) {
         double ey, ef;
         edge_solve(false, v1, L0, U0, need1, ey, ef);
@@ -1442,15 +1486,37 @@ template <int K, typename T>
 __device__ __forceinline__ void uni_qp_2d_core(double p0, double p1, double p2, double ip0, double ip1,
                                                const T* a0, const T* a1, const T* b, double L0, double U0,
                                                double L1, double U1, bool finite, double* z, int& status) {
+    RCBF_QP_STAMP(0);
     unsigned mask = 0;
+    if constexpr (sizeof(T) == 4 && RCBF_MASK32) {
+        // the raw fp32 rows (uni_qp_2d_raw): the bounds are fp32 values too,
+        // so the test runs in fp32 with a conservative margin.  The rounded
+        // m is within 3u S of the exact e_max (u = 2^-24, S the sum of the
+        // terms' magnitudes) and the margin is 8u S (plus an underflow
+        // floor), so a row is dropped only when its exact e_max < 0; keeping
+        // an extra row is the unpruned problem, hence harmless.  NaN: live.
+        const float l0 = (float)L0, u0 = (float)U0, l1 = (float)L1, u1 = (float)U1;
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const double x0 = (double)a0[j], x1 = (double)a1[j];
-        const double emax = (double)b[j] + fmax(x0 * L0, x0 * U0) + fmax(x1 * L1, x1 * U1);
-        mask |= (emax <= 0.0 ? 0u : 1u) << j;
+        for (int j = 0; j < K; ++j) {
+            const float x0 = (float)a0[j], x1 = (float)a1[j], bj = (float)b[j];
+            const float t0 = fmaxf(x0 * l0, x0 * u0), t1 = fmaxf(x1 * l1, x1 * u1);
+            const float m = (bj + t0) + t1;
+            const float sa = (fabsf(bj) + fabsf(t0)) + fabsf(t1);
+            mask |= (fmaf(0x1p-21f, sa, m) <= -0x1p-120f ? 0u : 1u) << j;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const double x0 = (double)a0[j], x1 = (double)a1[j];
+            const double emax = (double)b[j] + fmax(x0 * L0, x0 * U0) + fmax(x1 * L1, x1 * U1);
+            mask |= (emax <= 0.0 ? 0u : 1u) << j;
+        }
     }
     double bu0, bu1, bf, e;
     const int kmax = wave_max_count<K>(__popc(mask));
+    RCBF_QP_COUNT(8, kmax > 0);
+    RCBF_QP_COUNT(10, kmax > 1);
+    RCBF_QP_COUNT(11, kmax > 2);
     if (kmax == 0) {  // no hazard row can bind anywhere in the box, for every lane of the wave
         bu0 = fmin(fmax(0.0, L0), U0);
         bu1 = fmin(fmax(0.0, L1), U1);
@@ -1470,6 +1536,7 @@ __device__ __forceinline__ void uni_qp_2d_core(double p0, double p1, double p2, 
     z[0] = bu0;
     z[1] = bu1;
     z[2] = e;
+    RCBF_QP_STAMP(9);
     finite = finite && isfinite(U0 + L0 + U1 + L1);  // fmin/fmax would hide a NaN bound
     const bool ok = isfinite(z[0]) && isfinite(z[1]) && isfinite(z[2]) && bf < __builtin_huge_val();
     status = !finite ? RCBF_QP_NONFINITE : (ok && L0 <= U0 && L1 <= U1 ? RCBF_QP_OK : RCBF_QP_INFEASIBLE);

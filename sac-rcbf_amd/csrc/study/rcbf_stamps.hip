@@ -2,7 +2,11 @@
 // safe step instantiated with phase timestamps (Stamps<true>, s_memtime per
 // wave at phase boundaries), for scripts/stamps.py.  Built on demand into
 // build/study/librcbf_stamps.so; the product kernel is the same template with
-// the stamps compiled out.
+// the stamps compiled out.  RCBF_STUDY_QP_STAMPS adds the unicycle QP's
+// per-stage record (rcbf_device.hpp) into a second buffer.
+#define RCBF_STUDY_QP_STAMPS 1
+#include <hip/hip_runtime.h>
+__device__ unsigned long long* rcbf_qp_stamp_buf = nullptr;
 #include "../rcbf_safe_step.hpp"
 
 using namespace rcbf;
@@ -18,4 +22,9 @@ extern "C" int rcbf_study_safe_step_stamps(const rcbf_params* prm, int64_t B, do
                                           reward, cost, done, nullptr, nullptr, nullptr, auto_reset, seed, (int64_t)0,
                                           *prm, 0, stamps));
     return launch_status();
+}
+
+// the QP record's buffer (16 words per wave; null: off)
+extern "C" int rcbf_study_set_qp_stamps(unsigned long long* buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(rcbf_qp_stamp_buf), &buf, sizeof(buf));
 }

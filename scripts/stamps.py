@@ -55,6 +55,11 @@ slib = ctypes.CDLL(STUDY_LIB)
 P = ctypes.c_void_p
 slib.rcbf_study_safe_step_stamps.argtypes = [ctypes.POINTER(_lib.RcbfParams), ctypes.c_int64] + [P] * 11 + [
     ctypes.c_int32, ctypes.c_uint64, P]
+# the unicycle QP's per-stage record (rcbf_device.hpp RCBF_QP_STAMP / RCBF_QP_COUNT)
+qst = torch.zeros(nw * 16, dtype=torch.int64, device="cuda")
+slib.rcbf_study_set_qp_stamps.argtypes = [P]
+assert slib.rcbf_study_set_qp_stamps(_lib.ptr(qst) if uni else None) == 0
+qres, qcnt = [], []
 names = ["load", "get_state", "rows+norm", "QP", "env step", "obs+stores issued", "stores drained"]
 res, real = [], []
 fbs = []
@@ -93,6 +98,10 @@ for rep in range(30):
         rt = rt[(rt > 0).all(1)]
         real.append((rt[:, 1].max() - rt[:, 0].min(), np.percentile(rt[:, 0] - rt[:, 0].min(), 50),
                      rt[:, 0].max() - rt[:, 0].min(), np.percentile(rt[:, 1] - rt[:, 0], 50)))
+        if uni:
+            q = qst.view(nw, 16).cpu().numpy().astype(np.int64)
+            qres.append(np.diff(q[:, [0, 1, 2, 3, 4, 9]], axis=1))
+            qcnt.append(q[:, [5, 6, 7, 8, 10, 11]])
         fb = st.view(nw, 16)[:, 9].cpu().numpy()
         fbs = fbs + [fb] if rep > 10 else [fb]
 d = np.concatenate(res)
@@ -107,3 +116,18 @@ rl = np.array(real) * 0.01  # s_memrealtime ticks (100 MHz) -> us
 print(f"  chip clock (s_memrealtime, us, median over launches): first wave start -> last wave end {np.median(rl[:, 0]):.2f}; "
       f"wave start offsets median {np.median(rl[:, 1]):.2f}, last {np.median(rl[:, 2]):.2f}; wave lifetime median "
       f"{np.median(rl[:, 3]):.2f}")
+if uni:
+    qd = np.concatenate(qres)
+    qc = np.concatenate(qcnt)
+    live = qc[:, 3] > 0  # waves that ran the piecewise solver (the others skip slots 1-7: stale in graph replays)
+    print(f"  waves with a live hazard row: {live.mean():.4f}; with KK >= 2: {(qc[:, 4] > 0).mean():.4f}, KK >= 3: "
+          f"{(qc[:, 5] > 0).mean():.4f}")
+    qd, qc = qd[live], qc[live]
+    qn = ["mask + wave max + slots", "stage 1a (u = 0, pieces)", "stage 1b (kinks, triples)", "stage 2 u0-edge",
+          "stage 2 u1-edge"]
+    print("  unicycle QP stages, waves with a live row (ticks per wave, median / p90 / mean; the stamps' scheduling barriers included):")
+    for k, n in enumerate(qn):
+        print(f"    {n:26s} {np.median(qd[:, k]):8.0f} {np.percentile(qd[:, k], 90):8.0f} {qd[:, k].mean():8.0f}")
+    print(f"    {'QP total':26s} {np.median(qd.sum(1)):8.0f} {np.percentile(qd.sum(1), 90):8.0f} {qd.sum(1).mean():8.0f}")
+    for j, n in ((0, "open after stage 1a (run 1b)"), (1, "need the u0-edge"), (2, "need the u1-edge")):
+        print(f"  lanes {n}: {qc[:, j].sum() / (64 * qc.shape[0]):.4f} of lanes; waves with any: {(qc[:, j] > 0).mean():.4f}")
