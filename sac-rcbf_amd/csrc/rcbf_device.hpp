@@ -23,11 +23,6 @@ namespace rcbf {
 
 constexpr double kInf = __builtin_huge_val();
 
-// 1: the unicycle QP's live-row test in fp32 with a conservative margin
-// (uni_qp_2d_core); 0: in fp64
-#ifndef RCBF_MASK32
-#define RCBF_MASK32 0
-#endif
 #ifndef RCBF_STUDY_NO_EDGE2
 #define RCBF_STUDY_NO_EDGE2 0
 #endif
@@ -1400,7 +1395,10 @@ __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2
     // u1-edge (where u_f1 leaves [L1, U1]), each only in waves with such a lane
     const double v0 = fmin(fmax(bu0, L0), U0), v1 = fmin(fmax(bu1, L1), U1);
     bf = inbox ? bf : __builtin_huge_val();  // an out-of-box stage-1 point must not win
-#if RCBF_STUDY_NO_EDGE2  // timing ablation only: wrong results
+#if RCBF_STUDY_NO_EDGE2  // timing ablation only: wrong results (the clamped stage-1 point)
+    bu0 = v0;
+    bu1 = v1;
+    bf = 0.0;
     return;
 #endif
     if (__ballot(need0) != 0) {
@@ -1488,29 +1486,11 @@ __device__ __forceinline__ void uni_qp_2d_core(double p0, double p1, double p2, 
                                                double L1, double U1, bool finite, double* z, int& status) {
     RCBF_QP_STAMP(0);
     unsigned mask = 0;
-    if constexpr (sizeof(T) == 4 && RCBF_MASK32) {
-        // the raw fp32 rows (uni_qp_2d_raw): the bounds are fp32 values too,
-        // so the test runs in fp32 with a conservative margin.  The rounded
-        // m is within 3u S of the exact e_max (u = 2^-24, S the sum of the
-        // terms' magnitudes) and the margin is 8u S (plus an underflow
-        // floor), so a row is dropped only when its exact e_max < 0; keeping
-        // an extra row is the unpruned problem, hence harmless.  NaN: live.
-        const float l0 = (float)L0, u0 = (float)U0, l1 = (float)L1, u1 = (float)U1;
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const float x0 = (float)a0[j], x1 = (float)a1[j], bj = (float)b[j];
-            const float t0 = fmaxf(x0 * l0, x0 * u0), t1 = fmaxf(x1 * l1, x1 * u1);
-            const float m = (bj + t0) + t1;
-            const float sa = (fabsf(bj) + fabsf(t0)) + fabsf(t1);
-            mask |= (fmaf(0x1p-21f, sa, m) <= -0x1p-120f ? 0u : 1u) << j;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const double x0 = (double)a0[j], x1 = (double)a1[j];
-            const double emax = (double)b[j] + fmax(x0 * L0, x0 * U0) + fmax(x1 * L1, x1 * U1);
-            mask |= (emax <= 0.0 ? 0u : 1u) << j;
-        }
+    for (int j = 0; j < K; ++j) {
+        const double x0 = (double)a0[j], x1 = (double)a1[j];
+        const double emax = (double)b[j] + fmax(x0 * L0, x0 * U0) + fmax(x1 * L1, x1 * U1);
+        mask |= (emax <= 0.0 ? 0u : 1u) << j;
     }
     double bu0, bu1, bf, e;
     const int kmax = wave_max_count<K>(__popc(mask));

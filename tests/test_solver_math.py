@@ -136,65 +136,6 @@ def test_uni_pruning_on_the_bench_distribution(K):
     assert w["open"] < 0.5 and w["edge_open"] < 0.5, w
 
 
-def _live32(a0, a1, b, l0, u0, l1, u1):
-    """rcbf_device.hpp uni_qp_2d_core's fp32 live-row test (RCBF_MASK32),
-    restated in numpy fp32 (fmaf's 2^-21 s is exact, the final add rounds
-    once in fp64 then in fp32)."""
-    f = np.float32
-    with np.errstate(over="ignore", invalid="ignore"):
-        t0 = np.maximum(a0 * l0, a0 * u0).astype(f)
-        t1 = np.maximum(a1 * l1, a1 * u1).astype(f)
-        m = ((b + t0).astype(f) + t1).astype(f)
-        sa = ((np.abs(b) + np.abs(t0)).astype(f) + np.abs(t1)).astype(f)
-        v = (sa.astype(np.float64) * 2.0 ** -21 + m.astype(np.float64)).astype(f)
-        return ~(v <= f(-2.0 ** -120))
-
-
-def test_uni_live_row_test_fp32_is_conservative():
-    """The fp32 live-row test drops a hazard row only when its exact maximum
-    over the box, b + max(a0 l0, a0 u0) + max(a1 l1, a1 u1), is negative
-    (keeping an extra row is the unpruned problem, so only drops matter):
-    random fp32 rows and bounds, rows placed within a few ulps of the
-    boundary, tiny magnitudes, and non-finite entries (NaN keeps the row)."""
-    from fractions import Fraction
-    rng = np.random.default_rng(77)
-    f = np.float32
-    n = 200_000
-    a0 = (rng.standard_normal(n) * 10 ** rng.uniform(-3, 3, n)).astype(f)
-    a1 = (rng.standard_normal(n) * 10 ** rng.uniform(-3, 3, n)).astype(f)
-    l0, u0 = f(-1.3), f(2.7)
-    l1, u1 = f(-3.1), f(0.4)
-    d = np.maximum(a0.astype(np.float64) * l0, a0.astype(np.float64) * u0) + \
-        np.maximum(a1.astype(np.float64) * l1, a1.astype(np.float64) * u1)
-    # half the rows: b = -(the box maximum) nudged either way, so the exact maximum sits near 0
-    b = (rng.standard_normal(n) * 10 ** rng.uniform(-3, 3, n)).astype(f)
-    near = rng.random(n) < 0.5
-    # relative offsets of +-2e-6 (~ +-34 fp32 ulps) straddle the margin (16 u ~ 1e-6 of |d| here)
-    bn = (-d * (1 + rng.uniform(-2e-6, 2e-6, n))).astype(f)
-    b = np.where(near, bn, b)
-    live = _live32(a0, a1, b, l0, u0, l1, u1)
-    # every dropped row: the exact sign of its maximum over the box (Fractions)
-    F_ = lambda v: Fraction(float(v))  # noqa: E731
-    for i in np.nonzero(~live)[0]:
-        e = (F_(b[i]) + max(F_(a0[i]) * F_(l0), F_(a0[i]) * F_(u0))
-             + max(F_(a1[i]) * F_(l1), F_(a1[i]) * F_(u1)))
-        assert e < 0, (i, float(e))
-    # the near-boundary rows exercise both outcomes
-    assert 0.1 < live[near].mean() < 0.9
-    # tiny magnitudes (products underflow) and zeros: never dropped when the exact maximum is >= 0
-    z = np.zeros(4, f)
-    assert _live32(z, z, z, l0, u0, l1, u1).all()
-    tiny = np.full(4, f(1e-30))
-    assert _live32(tiny, tiny, -tiny * f(0.5), l0, u0, l1, u1).all()
-    # NaN data keeps the row (the lane fails later with the reference's exception)
-    nan = np.array([np.nan], f)
-    one = np.array([1.0], f)
-    assert _live32(nan, one, one, l0, u0, l1, u1).all() and _live32(one, one, nan, l0, u0, l1, u1).all()
-    # an infinite positive offset keeps the row (an infinite negative one gives inf - inf = NaN in
-    # the margin and is kept too: conservative; such a lane fails the finiteness check anyway)
-    assert _live32(one, one, np.array([np.inf], f), l0, u0, l1, u1).all()
-
-
 def _fma(a, b, c):
     """fma emulated in x87 extended precision (64-bit significand): within
     an ulp of the fused result, enough for a statistics test."""
