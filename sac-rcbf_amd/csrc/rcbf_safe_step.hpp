@@ -118,10 +118,20 @@ __device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_
     constexpr int CH = NO * 16;  // 16-byte chunks in the wave's block
     const float4* src = reinterpret_cast<const float4*>(lds_wave);
     float* dst = obs + base * NO;
+    // every chunk read from LDS first, then the stores: the write-through
+    // store is an asm with a memory clobber, which would otherwise hold each
+    // following LDS read (and its wait) behind the previous store
+    constexpr int NJ = (CH + 63) / 64;
+    float4 chunk[NJ];
 #pragma unroll
-    for (int j = 0; j < (CH + 63) / 64; ++j) {
+    for (int j = 0; j < NJ; ++j) {
         const int c = j * 64 + lane;
-        if (CH % 64 == 0 || c < CH) st_out4<MODE == RCBF_MODE_SIMULATED_CARS>(dst + 4 * c, src[c]);
+        if (CH % 64 == 0 || c < CH) chunk[j] = src[c];
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = j * 64 + lane;
+        if (CH % 64 == 0 || c < CH) st_out4<MODE == RCBF_MODE_SIMULATED_CARS>(dst + 4 * c, chunk[j]);
     }
 }
 
