@@ -17,6 +17,11 @@
 #ifndef RCBF_KARG_PREFETCH
 #define RCBF_KARG_PREFETCH 0
 #endif
+// 1: the cars step stores the state pairs that do not depend on the safe
+// action before the layer's chain ends (k_safe_step)
+#ifndef RCBF_EARLY_STORE
+#define RCBF_EARLY_STORE 1
+#endif
 
 namespace rcbf {
 
@@ -81,6 +86,33 @@ __device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double*
     }
 }
 
+// The wave's staged observation block (64 rows in LDS) to HBM as 16-byte
+// chunks, chunk c by lane c % 64.  Every chunk is read from LDS first, then
+// stored: the write-through store is an asm with a memory clobber, which
+// would otherwise hold each following LDS read (and its wait) behind the
+// previous store.
+template <int MODE>
+__device__ __forceinline__ void store_obs_chunks(float* obs, int64_t base, const float* lds_wave) {
+    constexpr int NO = Dims<MODE, 1>::NO;
+    const int lane = threadIdx.x & 63;
+    __builtin_amdgcn_wave_barrier();
+    constexpr int CH = NO * 16;  // 16-byte chunks in the wave's block
+    const float4* src = reinterpret_cast<const float4*>(lds_wave);
+    float* dst = obs + base * NO;
+    constexpr int NJ = (CH + 63) / 64;
+    float4 chunk[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = j * 64 + lane;
+        if (CH % 64 == 0 || c < CH) chunk[j] = src[c];
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = j * 64 + lane;
+        if (CH % 64 == 0 || c < CH) st_out4<MODE == RCBF_MODE_SIMULATED_CARS>(dst + 4 * c, chunk[j]);
+    }
+}
+
 // Observation store through LDS: a full wave's 64 obs rows are one
 // contiguous (64*NO*4)-byte block; lanes write their rows into LDS, then
 // store the block as 16-byte chunks, chunk c by lane c%64 -- every store
@@ -114,25 +146,7 @@ __device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_
 #pragma unroll
         for (int k = 0; k < NO; ++k) lds_wave[lane * NO + k] = (float)o[k];
     }
-    __builtin_amdgcn_wave_barrier();
-    constexpr int CH = NO * 16;  // 16-byte chunks in the wave's block
-    const float4* src = reinterpret_cast<const float4*>(lds_wave);
-    float* dst = obs + base * NO;
-    // every chunk read from LDS first, then the stores: the write-through
-    // store is an asm with a memory clobber, which would otherwise hold each
-    // following LDS read (and its wait) behind the previous store
-    constexpr int NJ = (CH + 63) / 64;
-    float4 chunk[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int c = j * 64 + lane;
-        if (CH % 64 == 0 || c < CH) chunk[j] = src[c];
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int c = j * 64 + lane;
-        if (CH % 64 == 0 || c < CH) st_out4<MODE == RCBF_MODE_SIMULATED_CARS>(dst + 4 * c, chunk[j]);
-    }
+    store_obs_chunks<MODE>(obs, base, lds_wave);
 }
 
 // The fused safe step (rcbf_safe_step): one env per lane.  ST = true only in
@@ -210,13 +224,74 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
     int status;
     stamps.mark(1, true);
     double oc[4] = {0.0, 0.0, 0.0, 0.0};
-    safe_step_one<SOLVER, MODE, K, ST>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status, auto_reset,
-                                       seed, off, stamps, oc, ep_pre, ep0);
-    store_state<MODE>(x, B, i, xs);
-    st_out(&aux[i], a);
-    st_out(&step[i], st);
     __shared__ float obs_stage[kBlock / 64][64 * D::NO];
-    store_obs32_staged<MODE>(obs_out, i, B, xs, oc, obs_stage[threadIdx.x >> 6]);
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && RCBF_EARLY_STORE && !ST) {
+        // The same step in an order that lets 76 of the 145 written bytes
+        // leave while the layer's chain is still running: the env's
+        // pre-step part (everything but car 3's velocity, t, step, done,
+        // cost) and the auto-reset do not depend on the safe action, so
+        // they, and the stores of state pairs 0, 1, 2, 4, t and step, come
+        // first; the layer's chain (state32 -> rows -> QP -> clamp) then
+        // finishes car 3's velocity (pair 3) and the observation.
+        float s32[D::NS];
+        state_from_env<MODE>(xs, s32);  // the layer reads the pre-step state
+        CarsStepOut o;
+        const double acc3 = cars_env_pre(prm, xs, a, st, o);
+        dn = o.done;
+        cst = (float)o.cost;
+        gm = false;
+        const bool rs = auto_reset && dn;
+        if (rs) {
+            const uint32_t ep = episode ? (ep_pre ? ep0 : episode[i]) + 1u : 0u;
+            if (episode) episode[i] = ep;
+            env_reset_one<MODE>(nullptr, i, seed, off, ep, xs, a, st);
+        }
+#pragma unroll
+        for (int p = 0; p < D::NS / 2; ++p)
+            if (p != 3) st_out2d(&x[2 * (p * B + i)], xs[2 * p], xs[2 * p + 1]);
+        st_out(&aux[i], a);
+        st_out(&step[i], st);
+        // RCBF_EARLY_STORE 2: the observation of every component but car
+        // 3's velocity (obs[7]) is final here too; it goes to the wave's LDS
+        // block now, and only obs[7] follows the layer's chain
+        const int lane = threadIdx.x & 63;
+        const bool staged = RCBF_EARLY_STORE >= 2 && (i - lane + 64 <= B) &&
+                            ((reinterpret_cast<uintptr_t>(obs_out) & 15) == 0);
+        float* lw = obs_stage[threadIdx.x >> 6];
+        if (staged) {
+            double o[D::NO];
+            cars_obs(xs, o);
+#pragma unroll
+            for (int k = 0; k < D::NO / 2; ++k)
+                if (k != 3)
+                    *reinterpret_cast<float2*>(&lw[lane * D::NO + 2 * k]) =
+                        make_float2((float)o[2 * k], (float)o[2 * k + 1]);
+            lw[lane * D::NO + 6] = (float)o[6];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the early stores ahead of the layer's chain
+        LayerState<MODE, K> L;
+        layer_forward<SOLVER, MODE, K, false, false, RCBF_FUSED_RAW_ROWS != 0>(prm, s32, us, m, s, uf, L);
+        status = L.qp.status;
+        const double v3_reset = xs[7];
+        cars_env_post<float>(xs, acc3, uf[0], o);  // car 3's velocity and the reward
+        xs[7] = rs ? v3_reset : xs[7];
+        rew = o.reward;
+        st_out2d(&x[2 * (3 * B + i)], xs[6], xs[7]);
+        if (staged) {
+            lw[lane * D::NO + 7] = (float)div_const(xs[7], 30.0, 1.0 / 30.0);  // obs[1::2] /= 30 (:157)
+            store_obs_chunks<MODE>(obs_out, i - lane, lw);
+        } else if (RCBF_EARLY_STORE >= 2) {
+            store_obs32<MODE>(obs_out, i, xs, oc);
+        }
+    } else {
+        safe_step_one<SOLVER, MODE, K, ST>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status,
+                                           auto_reset, seed, off, stamps, oc, ep_pre, ep0);
+        store_state<MODE>(x, B, i, xs);
+        st_out(&aux[i], a);
+        st_out(&step[i], st);
+    }
+    if (!(MODE == RCBF_MODE_SIMULATED_CARS && RCBF_EARLY_STORE >= 2 && !ST))
+        store_obs32_staged<MODE>(obs_out, i, B, xs, oc, obs_stage[threadIdx.x >> 6]);
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
     st_out(&reward[i], rew);
