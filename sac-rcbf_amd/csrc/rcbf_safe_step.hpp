@@ -18,7 +18,8 @@
 #define RCBF_KARG_PREFETCH 0
 #endif
 // 1: the cars step stores the state pairs that do not depend on the safe
-// action before the layer's chain ends (k_safe_step)
+// action before the layer's chain runs (k_safe_step; 3.86 -> 3.67 us per
+// step, profiles/r03/early_store_confirm_r03k.txt); 0: after it
 #ifndef RCBF_EARLY_STORE
 #define RCBF_EARLY_STORE 1
 #endif
@@ -224,7 +225,6 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
     int status;
     stamps.mark(1, true);
     double oc[4] = {0.0, 0.0, 0.0, 0.0};
-    __shared__ float obs_stage[kBlock / 64][64 * D::NO];
     if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && RCBF_EARLY_STORE && !ST) {
         // The same step in an order that lets 76 of the 145 written bytes
         // leave while the layer's chain is still running: the env's
@@ -251,23 +251,6 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
             if (p != 3) st_out2d(&x[2 * (p * B + i)], xs[2 * p], xs[2 * p + 1]);
         st_out(&aux[i], a);
         st_out(&step[i], st);
-        // RCBF_EARLY_STORE 2: the observation of every component but car
-        // 3's velocity (obs[7]) is final here too; it goes to the wave's LDS
-        // block now, and only obs[7] follows the layer's chain
-        const int lane = threadIdx.x & 63;
-        const bool staged = RCBF_EARLY_STORE >= 2 && (i - lane + 64 <= B) &&
-                            ((reinterpret_cast<uintptr_t>(obs_out) & 15) == 0);
-        float* lw = obs_stage[threadIdx.x >> 6];
-        if (staged) {
-            double o[D::NO];
-            cars_obs(xs, o);
-#pragma unroll
-            for (int k = 0; k < D::NO / 2; ++k)
-                if (k != 3)
-                    *reinterpret_cast<float2*>(&lw[lane * D::NO + 2 * k]) =
-                        make_float2((float)o[2 * k], (float)o[2 * k + 1]);
-            lw[lane * D::NO + 6] = (float)o[6];
-        }
         __builtin_amdgcn_sched_barrier(0);  // keep the early stores ahead of the layer's chain
         LayerState<MODE, K> L;
         layer_forward<SOLVER, MODE, K, false, false, RCBF_FUSED_RAW_ROWS != 0>(prm, s32, us, m, s, uf, L);
@@ -277,12 +260,6 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
         xs[7] = rs ? v3_reset : xs[7];
         rew = o.reward;
         st_out2d(&x[2 * (3 * B + i)], xs[6], xs[7]);
-        if (staged) {
-            lw[lane * D::NO + 7] = (float)div_const(xs[7], 30.0, 1.0 / 30.0);  // obs[1::2] /= 30 (:157)
-            store_obs_chunks<MODE>(obs_out, i - lane, lw);
-        } else if (RCBF_EARLY_STORE >= 2) {
-            store_obs32<MODE>(obs_out, i, xs, oc);
-        }
     } else {
         safe_step_one<SOLVER, MODE, K, ST>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status,
                                            auto_reset, seed, off, stamps, oc, ep_pre, ep0);
@@ -290,8 +267,8 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
         st_out(&aux[i], a);
         st_out(&step[i], st);
     }
-    if (!(MODE == RCBF_MODE_SIMULATED_CARS && RCBF_EARLY_STORE >= 2 && !ST))
-        store_obs32_staged<MODE>(obs_out, i, B, xs, oc, obs_stage[threadIdx.x >> 6]);
+    __shared__ float obs_stage[kBlock / 64][64 * D::NO];
+    store_obs32_staged<MODE>(obs_out, i, B, xs, oc, obs_stage[threadIdx.x >> 6]);
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
     st_out(&reward[i], rew);
