@@ -267,11 +267,7 @@ template <int MODE>
 __device__ __forceinline__ void env_reset_one(const double* noise, int64_t i, uint64_t seed, int64_t off,
                                               uint32_t ep, double* xs, double& aux, int& st) {
     if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
-#if RCBF_STUDY_NORESET_DRAW  // timing ablation only: a constant reset draw
-        double nz = noise ? noise[i] : 0.0 * (double)ep;
-#else
         double nz = noise ? noise[i] : 0.5 * normal_draw(seed, (uint64_t)(off + i), ep);
-#endif
         cars_reset_state(xs, nz);
         aux = 0.0;
     } else {

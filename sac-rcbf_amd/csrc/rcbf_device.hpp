@@ -23,9 +23,6 @@ namespace rcbf {
 
 constexpr double kInf = __builtin_huge_val();
 
-#ifndef RCBF_STUDY_NO_EDGE2
-#define RCBF_STUDY_NO_EDGE2 0
-#endif
 
 // Study build only (csrc/study/rcbf_stamps.hip defines RCBF_STUDY_QP_STAMPS
 // and the buffer): a 16-word record per wave of the unicycle QP -- s_memtime
@@ -1395,12 +1392,6 @@ __device__ __forceinline__ void uni_pieces_solve(double p0, double p1, double p2
     // u1-edge (where u_f1 leaves [L1, U1]), each only in waves with such a lane
     const double v0 = fmin(fmax(bu0, L0), U0), v1 = fmin(fmax(bu1, L1), U1);
     bf = inbox ? bf : __builtin_huge_val();  // an out-of-box stage-1 point must not win
-#if RCBF_STUDY_NO_EDGE2  // timing ablation only: wrong results (the clamped stage-1 point)
-    bu0 = v0;
-    bu1 = v1;
-    bf = 0.0;
-    return;
-#endif
     if (__ballot(need0) != 0) {
         double ey, ef;
         edge_solve(true, v0, L1, U1, need0, ey, ef);
