@@ -235,6 +235,12 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
         // finishes car 3's velocity (pair 3) and the observation.
         float s32[D::NS];
         state_from_env<MODE>(xs, s32);  // the layer reads the pre-step state
+        // the exact solver on the raw rows: the rows are built here, ahead of
+        // the env's pre-step part, whose arithmetic can then fill their latency
+        // (3.69 -> 3.65 us per step, profiles/r03/rows_first_ab_r03q.txt)
+        constexpr bool kRowsFirst = SOLVER == RCBF_SOLVER_ACTIVE_SET && RCBF_FUSED_RAW_ROWS != 0;
+        LayerState<MODE, K> L;
+        if constexpr (kRowsFirst) diff_rows<MODE, K>(prm, s32, us, m, s, L.G, L.h, nullptr);
         CarsStepOut o;
         const double acc3 = cars_env_pre(prm, xs, a, st, o);
         dn = o.done;
@@ -252,8 +258,18 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
         st_out(&aux[i], a);
         st_out(&step[i], st);
         __builtin_amdgcn_sched_barrier(0);  // keep the early stores ahead of the layer's chain
-        LayerState<MODE, K> L;
-        layer_forward<SOLVER, MODE, K, false, false, RCBF_FUSED_RAW_ROWS != 0>(prm, s32, us, m, s, uf, L);
+        if constexpr (kRowsFirst) {
+            PMat<D::N, true> pm;
+            double pd[D::N];
+            diff_P<MODE>(pd);
+            pmat_set_diag<D::N>(pm, pd);
+            cars_qp_1d_raw<float>(pm, L.G, L.h, L.qp.z, L.qp.status);
+#pragma unroll
+            for (int c = 0; c < D::NU; ++c)  // torch.clamp (diff_cbf_qp.py:77)
+                uf[c] = fminf(fmaxf(us[c] + (float)L.qp.z[c], (float)prm.u_min[c]), (float)prm.u_max[c]);
+        } else {
+            layer_forward<SOLVER, MODE, K, false, false, RCBF_FUSED_RAW_ROWS != 0>(prm, s32, us, m, s, uf, L);
+        }
         status = L.qp.status;
         const double v3_reset = xs[7];
         cars_env_post<float>(xs, acc3, uf[0], o);  // car 3's velocity and the reward
