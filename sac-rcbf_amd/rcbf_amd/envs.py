@@ -361,9 +361,16 @@ class BatchedEnv:
 
             def p(t):
                 return 0 if t is None else t.data_ptr()
+            # the cars env never meets a goal (info['goal_met'] is always False,
+            # simulated_cars_env.py:85): its goal_met output is zero-filled once
+            # here and the kernel is not asked to write it every step
+            gm = o.get("goal_met")
+            if gm is not None and self.dynamics_mode == "SimulatedCars":
+                gm.zero_()
+                gm = None
             args = [ctypes.addressof(layer._prm), self.num_envs, p(self.x), p(self.aux), p(self.step_count),
                     p(self.episode), 0, 0, 0, p(self.obs), p(o["u"]), p(o["reward"]), p(o["cost"]), p(o["done"]),
-                    p(o.get("goal_met")), 0, p(self.fail_flag), int(auto_reset), self._rng_seed(), self.env_offset, 0]
+                    p(gm), 0, p(self.fail_flag), int(auto_reset), self._rng_seed(), self.env_offset, 0]
             ent = self._ss_cache[key] = (layer, o, args, [t for t in o.values() if t is not None], layer._prm)
         return ent[2]
 
