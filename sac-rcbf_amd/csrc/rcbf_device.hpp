@@ -2105,13 +2105,7 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
 // env, and this took the cars step at SURVEY start states from 5.3 to 4.9 us
 // (profiles/r01).  Statistically a N(0,1) draw (|z| <= 5.8 with 24-bit
 // uniforms); restated by oracle.normal_draw.
-// study switch: the draw as an out-of-line call (off the fused step's
-// instruction stream; profiles/r03/reset_draw_*), default inline
-#if RCBF_STUDY_DRAW_NOINLINE
-__device__ __attribute__((noinline)) double normal_draw(uint64_t seed, uint64_t env, uint32_t episode) {
-#else
 __device__ __forceinline__ double normal_draw(uint64_t seed, uint64_t env, uint32_t episode) {
-#endif
     uint32_t c[4] = {(uint32_t)env, (uint32_t)(env >> 32), episode, 0x5AFEu};
     philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
     // hardware fp32 transcendentals (v_log_f32, v_cos_f32 takes revolutions)
