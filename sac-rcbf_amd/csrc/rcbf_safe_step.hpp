@@ -23,9 +23,6 @@
 #ifndef RCBF_EARLY_STORE
 #define RCBF_EARLY_STORE 1
 #endif
-#ifndef RCBF_STUDY_RESET_UNLIKELY
-#define RCBF_STUDY_RESET_UNLIKELY 0
-#endif
 
 namespace rcbf {
 
@@ -250,11 +247,7 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
         cst = (float)o.cost;
         gm = false;
         const bool rs = auto_reset && dn;
-#if RCBF_STUDY_RESET_UNLIKELY
-        if (__builtin_expect(rs, false)) {  // block placement: the reset code out of the hot path's stream
-#else
         if (rs) {
-#endif
             const uint32_t ep = episode ? (ep_pre ? ep0 : episode[i]) + 1u : 0u;
             if (episode) episode[i] = ep;
             env_reset_one<MODE>(nullptr, i, seed, off, ep, xs, a, st);
