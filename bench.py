@@ -43,6 +43,8 @@ PRIOR_TENSOR_BYTES = {"SimulatedCars": 12, "Unicycle": 24}
 
 
 def bytes_per_step(args):
+    if args.workload == "sac_update":
+        return SAC_UPDATE_BYTES[args.env]
     return BYTES_PER_STEP[args.env] + (PRIOR_TENSOR_BYTES[args.env] if args.prior in ("tensor", "rows") else 0)
 
 
@@ -77,7 +79,25 @@ def parse():
                     help="(internal) print the CPU baselines as JSON and exit; never touches the GPU")
     ap.add_argument("--host-cores", type=int, default=4,
                     help="host cores per rank for the launch threads (0: no pinning)")
-    return ap.parse_args()
+    ap.add_argument("--config", type=int, default=0, choices=[0, 1, 2, 3, 4, 5],
+                    help="a BASELINE.json config (0: the headline, cars B = 65536 per GPU): 1 cars, one env; "
+                         "2 cars B = 4096; 3 unicycle (3 hazards) B = 4096; 4 cars B = 262144 split over the GPUs "
+                         "(strong); 5 cars B = 4096 SAC-update safe action, forward + backward")
+    ap.add_argument("--workload", default="step", choices=["step", "sac_update"],
+                    help="step: the fused safe step; sac_update: RCBF_SAC.get_safe_action on a replay batch "
+                         "forward + backward (rcbf_obs_safe_action + its backward, config 5)")
+    ap.add_argument("--no-span", action="store_true", help="skip the untimed in-kernel span measurement")
+    args = ap.parse_args()
+    preset = {1: dict(env="SimulatedCars", batch=1, workload="step"),
+              2: dict(env="SimulatedCars", batch=4096, workload="step"),
+              3: dict(env="Unicycle", hazards=3, batch=4096, workload="step"),
+              4: dict(env="SimulatedCars", batch=262144, scaling="strong", workload="step"),
+              5: dict(env="SimulatedCars", batch=4096, workload="sac_update")}.get(args.config, {})
+    for k, v in preset.items():
+        setattr(args, k, v)
+    if args.workload == "sac_update" and (args.prior != "prior" or args.launch != "graph" or args.no_graph):
+        raise SystemExit("--workload sac_update runs the prior, hipGraph-launched")
+    return args
 
 
 def largest_divisor_le(n, cap):
@@ -87,17 +107,19 @@ def largest_divisor_le(n, cap):
     return 1
 
 
-def cpu_baseline(env_name, hazards, seconds):
+def cpu_baseline(env_name, hazards, seconds, B=65536):
     """The C oracle's fused step (oracle/rcbf_oracle.c: build + exact QP +
     clamp + env step, OpenMP over envs) on this host's cores, on a bounded
-    sample of the same workload (65536 envs, prior mean/sigma), ~`seconds`
-    in total: first 1 thread, then all threads OMP_NUM_THREADS allows."""
+    sample of the same workload (B envs, prior mean/sigma), ~`seconds` in
+    total: first 1 thread, then all threads OMP_NUM_THREADS allows (1 thread
+    below 1024 envs, where a parallel region costs more than the step)."""
     from oracle import c_oracle as C
     from oracle import oracle as O
-    B = 65536
     rng = np.random.default_rng(0)
     hz = O.UNI["hazards"][:hazards] if env_name == "Unicycle" else None
     threads_all = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    if B < 1024:
+        threads_all = 1
 
     def run(threads, budget):
         if env_name == "SimulatedCars":
@@ -112,7 +134,7 @@ def cpu_baseline(env_name, hazards, seconds):
             C.safe_step(env_name, x, aux, st, u, 20.0, hazards=hz, threads=threads)
             n += 1
             el = time.perf_counter() - t0
-            if el >= budget or n >= 100000:
+            if el >= budget or n * B >= 100000 * 65536:
                 return n * B / el, n, el
 
     v1, n1, e1 = run(1, seconds * 0.25)
@@ -127,6 +149,42 @@ def cpu_baseline(env_name, hazards, seconds):
             "spread": [round(r, 1) for r in rates]}
 
 
+def cpu_sac_update(env_name, hazards, seconds, B):
+    """Config 5's CPU baseline: the numpy oracle's CBFQPLayer forward and its
+    gradient w.r.t. the action (oracle.safe_action_diff / _grad: the
+    reference's fp32 rows, normaliser, exact QP, clamp, implicit-KKT
+    backward) on B rows of observations, numpy on this host (`cores` is the
+    BLAS thread count numpy may use; the loops themselves are vectorised
+    numpy on one core)."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(3)
+    hz = O.UNI["hazards"][:hazards] if env_name == "Unicycle" else None
+    if env_name == "SimulatedCars":
+        x, _, _ = O.cars_reset(rng.normal(0, 0.5, B))
+        obs = O.cars_obs(x).astype(np.float32)
+        n_u = 1
+    else:
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        obs = O.uni_obs(x).astype(np.float32)
+        n_u = 2
+    s32 = O.get_state_f32(env_name, obs)
+    mu, sg = O.predict_disturbance_prior(env_name, B)
+    mu, sg = mu.astype(np.float32), sg.astype(np.float32)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        u = rng.uniform(-1, 1, (B, n_u)).astype(np.float32)
+        w = rng.normal(0, 1, (B, n_u)).astype(np.float32)
+        O.safe_action_diff(env_name, s32, u, mu, sg, 20.0, hazards=hz)
+        O.safe_action_diff_grad(env_name, s32, u, mu, sg, 20.0, w, hazards=hz)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(n * B / el, 1), "unit": "safe actions/s (forward + backward)", "cores": 1, "kind": "port",
+            "sample": f"numpy oracle CBFQPLayer forward + d/du backward (oracle/oracle.py safe_action_diff, "
+                      f"safe_action_diff_grad), {n} batches x {B} rows in {el:.1f} s"}
+
+
 def cpu_baselines_in_child(args):
     """Both CPU baselines in a fresh child process that has never touched the
     GPU and starts with this process's full CPU mask (its OpenMP and torch
@@ -134,21 +192,21 @@ def cpu_baselines_in_child(args):
     them).  The parent waits for the child's JSON line."""
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--env", args.env,
-           "--hazards", str(args.hazards), "--cpu-seconds", str(args.cpu_seconds)]
+           "--hazards", str(args.hazards), "--cpu-seconds", str(args.cpu_seconds), "--batch", str(args.batch),
+           "--workload", args.workload]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         raise RuntimeError(f"CPU baseline child failed ({r.returncode}): {r.stderr[-2000:]}")
     return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
 
 
-def cpu_reference_mode(env_name, hazards, seconds):
+def cpu_reference_mode(env_name, hazards, seconds, B=65536):
     """The reference's own CPU mode restated (oracle/torch_mirror.py): fp32
     rows, normaliser, qpth-style batched PDIPM in torch fp64 (eps 1e-4,
     notImprovedLim 10, capped at 100 iterations), clamp, numpy env step, on
-    the same 65536 envs, on the torch threads of this host."""
+    the same B envs, on the torch threads of this host."""
     from oracle import oracle as O
     from oracle import torch_mirror as M
-    B = 65536
     rng = np.random.default_rng(1)
     threads = torch.get_num_threads()
     if env_name == "SimulatedCars":
@@ -172,23 +230,6 @@ def cpu_reference_mode(env_name, hazards, seconds):
     return {"value": round(n * B / el, 1), "unit": "safe env steps/s", "cores": threads, "kind": "port",
             "sample": f"reference CPU mode restated (oracle/torch_mirror.py: torch-CPU qpth-style PDIPM, from seeded resets, "
                       f"{its / n:.1f} iterations per step), {n} steps x {B} envs in {el:.1f} s on {threads} threads"}
-
-
-def pmc_traffic(env_name, B, hazards=3, prior="prior"):
-    """HBM bytes per launch of k_safe_step from the committed rocprofv3 PMC
-    passes (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, gfx950
-    corrections) for this exact workload, newest round first; None if absent."""
-    import glob
-    short = ("cars" if env_name == "SimulatedCars" else f"unicycle{hazards}") + {"prior": "", "tensor": "_tensorprior",
-                                                                                 "rows": "_rowsprior"}[prior]
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{short}_B{B}.json")),
-                       reverse=True):
-        try:
-            rec = json.load(open(path))
-            return float(rec["traffic_bytes"]), os.path.relpath(path, ROOT)
-        except Exception:
-            continue
-    return None, None
 
 
 def init_states(env, gen, env_name):
@@ -286,12 +327,152 @@ def pin_host_cores(local, n):
     return set(allowed), plan[local]
 
 
+METRICS = {
+    0: "safe env steps/sec (dynamics+CBF-QP) at batch 65536, 1/2/4/8 MI355X",
+    1: "safe env steps/sec (dynamics+CBF-QP), config 1: SimulatedCars, 1 env",
+    2: "safe env steps/sec (dynamics+CBF-QP), config 2: SimulatedCars batch 4096, 1 MI355X",
+    3: "safe env steps/sec (dynamics+CBF-QP), config 3: Unicycle (3 hazards) batch 4096, 1 MI355X",
+    4: "safe env steps/sec (dynamics+CBF-QP), config 4: SimulatedCars batch 262144 over the GPUs",
+    5: "safe actions/sec (diff CBF-QP forward + backward), config 5: SimulatedCars batch 4096, 1 MI355X",
+}
+
+# Algorithmic bytes of one forward + backward of the SAC-update safe action
+# per row, prior mean/sigma (config 5): forward reads obs + u_RL, writes u;
+# backward reads obs + u_RL + grad_u, writes grad_u_RL.
+#   cars     fwd 40 + 4 + 4 = 48,  bwd 40 + 4 + 4 + 4 = 52  -> 100
+#   unicycle fwd 28 + 8 + 8 = 44,  bwd 28 + 8 + 8 + 8 = 52  ->  96
+SAC_UPDATE_BYTES = {"SimulatedCars": 100, "Unicycle": 96}
+
+
+def block_for_envs(B):
+    """Workgroup size of the one-env-per-lane kernels (rcbf_common.hpp
+    block_for_envs): 256 from 65 536 envs, 128 from 32 768, else 64."""
+    return 256 if B >= 256 * 256 else 128 if B >= 256 * 128 else 64
+
+
+def workload_short(args):
+    """The workload's name in profiles/ file names."""
+    base = "cars" if args.env == "SimulatedCars" else f"uni{args.hazards}"
+    if args.workload == "sac_update":
+        return "sacupd_" + base
+    return base + {"prior": "", "tensor": "_tensorprior", "rows": "_rowsprior"}[args.prior]
+
+
+def dominant_kernels(args, B):
+    """The kernel(s) one timed step launches, as rocprofv3 names them."""
+    solver = 1 if args.solver == "pdipm" else 0
+    mode, K = (0, 1) if args.env == "SimulatedCars" else (1, args.hazards)
+    bs = block_for_envs(B)
+    if args.workload == "sac_update":
+        return [f"k_safe_action<{solver}, {mode}, {K}, true, {bs}>", f"k_safe_action_bwd<{solver}, {mode}, {K}, true, {bs}>"]
+    return [f"k_safe_step<{solver}, {mode}, {K}, false, {bs}, false>"]
+
+
+def _profiles_newest(pattern):
+    """profiles/r*/<pattern> files, newest round (then run tag) first."""
+    import glob
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", pattern)), reverse=True)
+
+
+def pmc_traffic_file(short, B):
+    """HBM bytes per launch of the dominant kernel from the committed
+    rocprofv3 PMC passes (scripts/pmc_traffic.py: 2 x FETCH_SIZE +
+    WRITE_SIZE, gfx950 corrections) of this exact workload, newest first;
+    (None, None) if absent."""
+    for path in _profiles_newest(f"pmc_traffic_{short}_B{B}.json"):
+        try:
+            return float(json.load(open(path))["traffic_bytes"]), os.path.relpath(path, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
+def rocprof_kernel_us(short, B, kernels):
+    """Mean duration (us) of one timed step's kernels -- the sum of their
+    AverageNs -- from the newest committed rocprofv3 --kernel-trace --stats
+    summary of this workload (profiles/r*/kernel_stats_<short>_B<B>_<tag>.csv);
+    (None, None) if there is none."""
+    import csv
+    for path in _profiles_newest(f"kernel_stats_{short}_B{B}_*.csv"):
+        try:
+            rows = list(csv.DictReader(open(path)))
+            tot = 0.0
+            for k in kernels:
+                hit = [r for r in rows if k in r["Name"]]
+                if len(hit) != 1:
+                    raise KeyError(k)
+                tot += float(hit[0]["AverageNs"]) / 1e3
+            return round(tot, 4), os.path.relpath(path, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
+def measure_span(env, layer, ctx, dev, B, bps, n=100):
+    """Untimed, after the timed region: the kernel's own span, untraced.  A
+    hipGraph of n launches of rcbf_safe_step_span (the product kernel plus,
+    per wave, the 100 MHz chip clock at its start and after its stores have
+    landed) replayed twice; per launch, span = last wave end - first wave
+    start, period = next launch's first start - this one's, gap = next
+    launch's first start - this launch's last end (the dependent-kernel
+    boundary).  The span graph's own per-step time by HIP events is reported
+    beside it (the two stamps and a drain per wave)."""
+    nw = (B + 63) // 64
+    buf = torch.zeros(n, nw, 2, dtype=torch.int64, device=dev)
+    pool, mean, sigma, layout, outs = ctx["pool"], ctx["mean"], ctx["sigma"], ctx["layout"], ctx["outs"]
+
+    def launches():
+        for j in range(n):
+            env.safe_step_span(pool[j % len(pool)], layer, buf[j], mean=mean, sigma=sigma, outputs=outs,
+                               prior_layout=layout)
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        launches()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        launches()
+    g.replay()
+    torch.cuda.synchronize()
+    buf.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    env.check_failures()
+    ev_us = e0.elapsed_time(e1) * 1e3 / n
+    t = buf.cpu().numpy().astype(np.float64)
+    valid = t[:, :, 1] > 0
+    start = np.where(valid, t[:, :, 0], np.inf).min(1)
+    end = np.where(valid, t[:, :, 1], -np.inf).max(1)
+    span = (end - start) * 0.01  # 100 MHz ticks -> us
+    period = np.diff(start) * 0.01
+    gap = (start[1:] - end[:-1]) * 0.01
+    med = float(np.median(span))
+    return {"kernel_span_us_median": round(med, 3), "kernel_span_us_mean": round(float(span.mean()), 3),
+            "kernel_span_us_p10_p90": [round(float(np.percentile(span, 10)), 3),
+                                       round(float(np.percentile(span, 90)), 3)],
+            "period_us_median": round(float(np.median(period)), 3),
+            "boundary_gap_us_median": round(float(np.median(gap)), 3),
+            "span_build_events_us_per_step": round(ev_us, 3), "launches": n, "waves_per_launch": nw,
+            "frac_span": round(B * bps / (med * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "how": "rcbf_safe_step_span in a hipGraph of 100 launches, untraced: per launch the last wave's end "
+                   "(after its stores landed) minus the first wave's start, s_memrealtime (100 MHz chip clock); "
+                   "frac_span = bytes_per_launch / median span"}
+
+
 def main():
     args = parse()
     if args.cpu_baseline_only:
-        print(json.dumps({"cpu_baseline": cpu_baseline(args.env, args.hazards, args.cpu_seconds),
-                          "cpu_reference_mode": cpu_reference_mode(args.env, args.hazards, args.cpu_seconds / 3)}),
-              flush=True)
+        if args.workload == "sac_update":
+            out = {"cpu_baseline": cpu_sac_update(args.env, args.hazards, args.cpu_seconds, args.batch)}
+        else:
+            out = {"cpu_baseline": cpu_baseline(args.env, args.hazards, args.cpu_seconds, args.batch),
+                   "cpu_reference_mode": cpu_reference_mode(args.env, args.hazards, args.cpu_seconds / 3,
+                                                            args.batch)}
+        print(json.dumps(out), flush=True)
         return
     from rcbf_amd import shard
     rank, local, world = shard.world_info()
@@ -321,7 +502,8 @@ def main():
         dev = torch.device("cuda", local)
         if world > 1:
             dist.init_process_group("nccl", device_id=dev)
-        env, layer, graph, S, active_frac, untimed = setup_gpu(args, dev, rank, B)
+        setup = setup_sac_update if args.workload == "sac_update" else setup_gpu
+        env, layer, graph, S, active_frac, untimed, ctx = setup(args, dev, rank, B)
         reps = args.steps // S
         sync = torch.cuda.synchronize
 
@@ -359,17 +541,27 @@ def main():
     value = shard.whole_job_rate(world, B, args.steps, el)
     bps = bytes_per_step(args)
     achieved = B * bps / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(args.env, B, args.hazards, args.prior)
+    short = workload_short(args)
+    traffic, traffic_src = pmc_traffic_file(short, B)
+    kernels = dominant_kernels(args, B)
+    k_us_rp, rp_src = rocprof_kernel_us(short, B, kernels)
+    span = {}
+    if rank == 0 and not args.cpu_dry_run and not args.no_span and args.workload == "step":
+        span = measure_span(env, layer, ctx, dev, B, bps)
     extra = {}
-    if args.extra and rank == 0 and not args.cpu_dry_run:
+    if args.extra and rank == 0 and not args.cpu_dry_run and args.workload == "step":
         extra = extra_measurements(env, layer, dev, args)
     hz = f"{args.hazards}-hazard " if args.env == "Unicycle" else ""
     launch = ("no kernel (CPU dry run)" if args.cpu_dry_run else "eager launches" if args.no_graph
               else f"{S} launches from one host call" if args.launch == "seq" else f"hipGraph of {S} steps")
+    sac = args.workload == "sac_update"
+    what = ("RCBF_SAC.get_safe_action forward + backward on a replay batch (rcbf_obs_safe_action + "
+            "rcbf_obs_safe_action_backward, diff CBF-QP, implicit-KKT grad)" if sac else
+            "fused safe step (rcbf_safe_step), non-diff CBF-QP")
     rec = {
-        "metric": "safe env steps/sec (dynamics+CBF-QP) at batch 65536, 1/2/4/8 MI355X",
+        "metric": METRICS.get(args.config, METRICS[0]),
         "value": round(value, 1),
-        "unit": "safe env steps/s",
+        "unit": "safe actions/s (forward + backward)" if sac else "safe env steps/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -378,15 +570,16 @@ def main():
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "f32 rows / f64 QP / f64 env",
+        "dtype": "f32 rows / f64 QP" if sac else "f32 rows / f64 QP / f64 env",
         "data": ("dry run: launcher and collectives only, no kernel, not a measurement" if args.cpu_dry_run else
                  "synthetic (SURVEY 8(d) start states, u_RL ~ U[-1,1], "
                  + {"prior": "prior mean/sigma",
                     "tensor": "per-env mean/sigma, column layout of rcbf_gp_predict_cols (post-GP-fit regime)",
                     "rows": "per-env mean/sigma (B, n_s) row tensors (post-GP-fit regime)"}[args.prior]
                  + ", seeded auto-resets)"),
-        "config": {"workload": f"{args.env} fused safe step (rcbf_safe_step), non-diff CBF-QP, {hz}"
+        "config": {"workload": f"{args.env} {what}, {hz}"
                                f"batch {B} envs per GPU, {args.solver} fp64 QP, {launch}",
+                   "baseline_config": args.config or None,
                    "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
                    "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)",
                    "prior": args.prior, "qp_active_frac_at_start": round(active_frac, 4),
@@ -394,12 +587,20 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": "k_safe_step", "bytes_per_env_step": bps, "bytes_per_launch": B * bps,
+                     "kernel": " + ".join(kernels), "bytes_per_env_step": bps, "bytes_per_launch": B * bps,
                      "kernel_ms": round(kern_ms, 5), "host_submit_ms": round(t_sub * 1e3, 4),
+                     "kernel_us_rocprof": k_us_rp,
+                     "frac_rocprof": round(B * bps / (k_us_rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if k_us_rp else None,
+                     "rocprof_source": rp_src,
                      "timing": "achieved = bytes_per_launch / kernel_ms; kernel_ms = HIP events around the timed "
                                "region / steps (includes the graph launch and the inter-kernel gaps); host_submit_ms "
-                               "= host time spent in the graph replay calls"},
+                               "= host time spent in the graph replay calls; kernel_us_rocprof = the AverageNs of "
+                               "this kernel in rocprof_source (rocprofv3 --kernel-trace --stats of this command, a "
+                               "traced run: each dispatch serialised with its own completion signal); frac_rocprof "
+                               "= bytes_per_launch / kernel_us_rocprof"},
     }
+    if span:
+        rec["roofline"]["span"] = span
     if world > 1:  # the spread of the timed region over ranks (value is set by the slowest)
         ms = sorted(v / args.steps * 1e3 for v in per_rank_s)
         rec["per_rank_ms"] = {"min": round(ms[0], 5), "median": round(float(np.median(ms)), 5),
@@ -473,7 +674,7 @@ def setup_gpu(args, dev, rank, B):
     if args.launch == "seq" and not args.no_graph:
         class _Seq:
             def replay(self):
-                env.safe_step_seq(pool, layer, mean=mean, sigma=sigma, outputs=outs, steps=S)
+                env.safe_step_seq(pool, layer, mean=mean, sigma=sigma, outputs=outs, steps=S, prior_layout=layout)
         graph = _Seq()
         graph.replay()
         untimed += S
@@ -496,7 +697,76 @@ def setup_gpu(args, dev, rank, B):
         untimed += 2 + 2 * S
     torch.cuda.synchronize()
     env.check_failures()
-    return env, layer, graph, S, active_frac, untimed
+    ctx = {"pool": pool, "mean": mean, "sigma": sigma, "layout": layout, "outs": outs}
+    return env, layer, graph, S, active_frac, untimed, ctx
+
+
+def setup_sac_update(args, dev, rank, B):
+    """Untimed set-up of config 5: RCBF_SAC.get_safe_action as the SAC update
+    calls it on a replay batch (sac_cbf.py:133,149 -> :218-238): fp32
+    observations of SURVEY 8(d) start states, policy actions u ~ U[-1, 1]
+    (50 batches cycled), the prior, and an upstream gradient; one timed step
+    = rcbf_obs_safe_action + rcbf_obs_safe_action_backward over the batch,
+    S of them captured in one hipGraph."""
+    import ctypes
+    from rcbf_amd import _lib, shard
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+
+    class LArgs:
+        cuda = True
+    if args.env == "SimulatedCars":
+        env = BatchedSimulatedCarsEnv(B, device=dev, seed=1234, env_offset=shard.env_offset(rank, B))
+    else:
+        env = BatchedUnicycleEnv(B, device=dev, seed=1234, env_offset=shard.env_offset(rank, B),
+                                 hazards_locations=unicycle_hazards(args.hazards))
+    layer = CBFQPLayer(env, LArgs(), gamma_b=20.0)
+    lib = _lib.load()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2000 + rank)
+    init_states(env, gen, args.env)
+    obs = env.obs.clone()
+    S = largest_divisor_le(args.steps, args.graph_steps)
+    npool = min(S, 50)
+    us = [(torch.rand(B, env.n_u, device=dev, generator=gen) * 2 - 1).contiguous() for _ in range(npool)]
+    ws = [torch.randn(B, env.n_u, device=dev, generator=gen).contiguous() for _ in range(npool)]
+    uo = torch.empty(B, env.n_u, device=dev)
+    gu = torch.empty(B, env.n_u, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    prm = ctypes.byref(layer._prm)
+
+    def steps(n, off=0):
+        s = _lib.stream_of(dev)
+        for j in range(n):
+            k = (off + j) % npool
+            _lib.check(lib.rcbf_obs_safe_action(prm, B, _lib.ptr(obs), _lib.ptr(us[k]), None, None, _lib.ptr(uo),
+                                                None, _lib.ptr(flag), s), "rcbf_obs_safe_action")
+            _lib.check(lib.rcbf_obs_safe_action_backward(prm, B, _lib.ptr(obs), _lib.ptr(us[k]), None, None,
+                                                         _lib.ptr(ws[k]), _lib.ptr(gu), s),
+                       "rcbf_obs_safe_action_backward")
+    steps(1)
+    torch.cuda.synchronize()
+    active_frac = float((uo != us[0]).any(1).float().mean().item())
+    steps(max(args.warmup, 1))
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        steps(2)
+    torch.cuda.current_stream(dev).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        steps(S)
+    for _ in range(2):
+        graph.replay()
+    torch.cuda.synchronize()
+
+    class _Fails:
+        def check_failures(self):
+            if int(flag.item()):
+                raise Exception("QP Failed to solve")
+    _Fails().check_failures()
+    untimed = 1 + max(args.warmup, 1) + 2 + 2 * S
+    return _Fails(), layer, graph, S, active_frac, untimed, {}
 
 
 def sac_update_safe_action(env, layer, dev):

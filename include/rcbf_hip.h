@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 8
+#define RCBF_ABI_VERSION 9
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -372,6 +372,29 @@ int rcbf_safe_step_seq(const rcbf_params* prm, int64_t B, int32_t K, double* x, 
                        float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
                        int32_t* fail_flag, int32_t auto_reset, uint64_t seed, int64_t env_offset,
                        hipStream_t stream);
+
+/* rcbf_safe_step_seq with the disturbance prediction in the column layout
+ * of rcbf_safe_step_cols (same arguments and rules as that entry point). */
+int rcbf_safe_step_seq_cols(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux,
+                            int32_t* step, uint32_t* episode, const float* const* u_rl_seq, int32_t n_u_rl,
+                            const float* mu_cols, const float* sigma_cols, float* obs_out, float* u_out,
+                            float* reward, float* cost, uint8_t* done, uint8_t* goal_met,
+                            int32_t* status_out, int32_t* fail_flag, int32_t auto_reset, uint64_t seed,
+                            int64_t env_offset, hipStream_t stream);
+
+/* MEASUREMENT entry point (bench.py's untraced kernel span; not a reference
+ * interface): rcbf_safe_step (prior_cols = 0) or rcbf_safe_step_cols
+ * (prior_cols = 1), the same instructions, plus per wavefront w (lanes
+ * 64w..64w+63 of the launch, w < ceil(B / 64)) lane 0 writes the 100 MHz chip
+ * clock (s_memrealtime) at the wave's start and after its own stores have
+ * completed: span_out[2w], span_out[2w+1] (uint64, 16-B aligned).  The
+ * launch's kernel span is max(end) - min(start) over its waves. */
+int rcbf_safe_step_span(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step,
+                        uint32_t* episode, const float* u_rl, const float* mu, const float* sigma,
+                        int32_t prior_cols, float* obs_out, float* u_out, float* reward, float* cost,
+                        uint8_t* done, uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag,
+                        int32_t auto_reset, uint64_t seed, int64_t env_offset, uint64_t* span_out,
+                        hipStream_t stream);
 
 /* K fused safe steps in ONE launch with the env state held in registers
  * (a pre-sampled u_rl (K, B, n_u), e.g. the reference's warm-up phase that

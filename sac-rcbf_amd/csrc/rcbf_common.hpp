@@ -22,7 +22,22 @@ inline unsigned grid_for(int64_t B) { return (unsigned)((B + kBlock - 1) / kBloc
 inline unsigned grid_for_envs(int64_t B) { return grid_for(B); }
 
 // env index of this lane in the env kernels: one env per lane
-__device__ __forceinline__ int64_t env_index() { return (int64_t)blockIdx.x * kBlock + threadIdx.x; }
+template <int BS = kBlock>
+__device__ __forceinline__ int64_t env_index() { return (int64_t)blockIdx.x * BS + threadIdx.x; }
+
+// Workgroup size of the fused step for a batch of B envs.  The step is a
+// per-CU memory-request-bound chain at one wave per SIMD (half
+// the batch on half the CUs takes the same time), so a batch that would leave
+// CUs without a 256-thread workgroup (B < 256 CUs x 256) is cut into smaller
+// workgroups that reach more CUs: 128 threads for B >= 32 768 (256-511
+// workgroups), 64 below (one wave per workgroup).
+constexpr int64_t kNumCU = 256;
+#ifndef RCBF_STUDY_BLOCK256  // study build: 256-thread workgroups at every batch (the r03 launch)
+inline int block_for_envs(int64_t B) { return B >= kNumCU * 256 ? 256 : B >= kNumCU * 128 ? 128 : 64; }
+#else
+inline int block_for_envs(int64_t) { return 256; }
+#endif
+inline unsigned grid_for_envs(int64_t B, int bs) { return (unsigned)((B + bs - 1) / bs); }
 
 // Memory policy of the env kernels: every once-read input is an `nt` load and
 // every output an `nt` store (with the whole-line stores below the fastest of
@@ -331,7 +346,12 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
     float cs_row[2];
     double c_th = 0.0, s_th = 0.0;  // unicycle: cos/sin of the pre-step theta, shared by obs, rows and env step
     if constexpr (MODE == RCBF_MODE_UNICYCLE) {
+#ifndef RCBF_STUDY_UNI_NO_SINCOS
         sincos(xs[2], &s_th, &c_th);
+#else  // study build, timing only (results invalid): the pre-step sincos replaced by a cheap stand-in
+        c_th = fma(-0.5 * xs[2], xs[2], 1.0);
+        s_th = xs[2];
+#endif
         uni_state32_from_cs(xs, c_th, s_th, s32, cs_row[0], cs_row[1]);
     } else {
         state_from_env<MODE>(xs, s32);
@@ -408,6 +428,23 @@ inline int check_prm(const rcbf_params* prm) {
 inline int launch_status() { return (int)hipGetLastError(); }
 
 }  // namespace rcbf
+
+// Launch KERNEL (a template-id naming BS_) over B envs at the workgroup size
+// block_for_envs(B): BS_ is 256, 128 or 64 in the three instantiations.
+#define RCBF_BS_LAUNCH(B, KERNEL, stream, ...)                                                                \
+    do {                                                                                                    \
+        const int bs_ = rcbf::block_for_envs(B);                                                            \
+        if (bs_ == 256) {                                                                                   \
+            constexpr int BS_ = 256;                                                                        \
+            hipLaunchKernelGGL(KERNEL, dim3(rcbf::grid_for_envs(B, BS_)), dim3(BS_), 0, stream, __VA_ARGS__); \
+        } else if (bs_ == 128) {                                                                            \
+            constexpr int BS_ = 128;                                                                        \
+            hipLaunchKernelGGL(KERNEL, dim3(rcbf::grid_for_envs(B, BS_)), dim3(BS_), 0, stream, __VA_ARGS__); \
+        } else {                                                                                            \
+            constexpr int BS_ = 64;                                                                         \
+            hipLaunchKernelGGL(KERNEL, dim3(rcbf::grid_for_envs(B, BS_)), dim3(BS_), 0, stream, __VA_ARGS__); \
+        }                                                                                                   \
+    } while (0)
 
 // Dispatch a launch over (mode, unicycle hazard count) -> MODE_, K_.
 #define RCBF_DISPATCH_MODE(prm, ...)                                 \

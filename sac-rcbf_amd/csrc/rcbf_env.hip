@@ -289,20 +289,52 @@ int rcbf_host_free(void* ptr) { return ptr ? (int)hipHostFree(ptr) : 0; }
 
 namespace {
 
+// One fused-step launch of the instantiation <SOLVER, MODE, K> at the
+// workgroup size block_for_envs(B) picks; SPAN: the span-stamped entry point.
+template <int SOLVER, int MODE, int K, bool SPAN = false>
+void launch_k_safe_step(int64_t B, double* x, double* aux, int32_t* step, const float* u_rl, uint32_t* episode,
+                        const float* mu, const float* sigma, float* obs_out, float* u_out, float* reward,
+                        float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag,
+                        int32_t auto_reset, uint64_t seed, int64_t env_offset, const rcbf_params& prm, int cols,
+                        unsigned long long* span, hipStream_t stream) {
+    const int bs = block_for_envs(B);
+#define RCBF_SS_L(BS_)                                                                                             \
+    hipLaunchKernelGGL((k_safe_step<SOLVER, MODE, K, false, BS_, SPAN>), dim3(grid_for_envs(B, BS_)), dim3(BS_), 0, \
+                       stream, B, x, aux, step, u_rl, episode, mu, sigma, obs_out, u_out, reward, cost, done,       \
+                       goal_met, status_out, fail_flag, auto_reset, seed, env_offset, prm, cols, span)
+    if (bs == 256)
+        RCBF_SS_L(256);
+    else if (bs == 128)
+        RCBF_SS_L(128);
+    else
+        RCBF_SS_L(64);
+#undef RCBF_SS_L
+}
+
 int safe_step_launch(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
                      const float* u_rl, const float* mu, const float* sigma, float* obs_out, float* u_out,
                      float* reward, float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
                      int32_t* fail_flag, int32_t auto_reset, uint64_t seed, int64_t env_offset, int cols,
-                     hipStream_t stream) {
+                     unsigned long long* span, hipStream_t stream) {
     if (int e = check_prm(prm)) return e;
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !aux || !step || !u_rl || !obs_out || !u_out || !reward || !cost || !done) return RCBF_E_NULL;
     if ((((uintptr_t)obs_out) & 7) || (((uintptr_t)x) & 15)) return RCBF_E_BAD_SHAPE;  // 8/16-B accesses
-    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0,
-                                          stream, B, x, aux, step, u_rl, episode, mu, sigma, obs_out, u_out, reward,
-                                          cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset,
-                                          *prm, cols));
+    if (span) {  // the measurement entry point: the default (exact active-set) solver only
+        if (((uintptr_t)span) & 15) return RCBF_E_BAD_SHAPE;
+        if (prm->solver != RCBF_SOLVER_ACTIVE_SET) return RCBF_E_BAD_MODE;
+        constexpr int SOLVER_ = RCBF_SOLVER_ACTIVE_SET;
+        RCBF_DISPATCH_MODE(prm, (launch_k_safe_step<SOLVER_, MODE_, K_, true>(
+                                    B, x, aux, step, u_rl, episode, mu, sigma, obs_out, u_out, reward, cost, done,
+                                    goal_met, status_out, fail_flag, auto_reset, seed, env_offset, *prm, cols, span,
+                                    stream)));
+    } else {
+        RCBF_DISPATCH(prm, (launch_k_safe_step<SOLVER_, MODE_, K_>(B, x, aux, step, u_rl, episode, mu, sigma, obs_out,
+                                                                   u_out, reward, cost, done, goal_met, status_out,
+                                                                   fail_flag, auto_reset, seed, env_offset, *prm, cols,
+                                                                   nullptr, stream)));
+    }
     return launch_status();
 }
 
@@ -315,7 +347,19 @@ int rcbf_safe_step(const rcbf_params* prm, int64_t B, double* x, double* aux, in
                    float* reward, float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
                    int32_t* fail_flag, int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream) {
     return safe_step_launch(prm, B, x, aux, step, episode, u_rl, mu, sigma, obs_out, u_out, reward, cost, done,
-                            goal_met, status_out, fail_flag, auto_reset, seed, env_offset, 0, stream);
+                            goal_met, status_out, fail_flag, auto_reset, seed, env_offset, 0, nullptr, stream);
+}
+
+int rcbf_safe_step_span(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
+                        const float* u_rl, const float* mu, const float* sigma, int32_t prior_cols, float* obs_out,
+                        float* u_out, float* reward, float* cost, uint8_t* done, uint8_t* goal_met,
+                        int32_t* status_out, int32_t* fail_flag, int32_t auto_reset, uint64_t seed,
+                        int64_t env_offset, uint64_t* span_out, hipStream_t stream) {
+    if (!span_out) return RCBF_E_NULL;
+    if (prior_cols && prm && prm->mode == RCBF_MODE_SIMULATED_CARS && mu) return RCBF_E_BAD_SHAPE;
+    return safe_step_launch(prm, B, x, aux, step, episode, u_rl, mu, sigma, obs_out, u_out, reward, cost, done,
+                            goal_met, status_out, fail_flag, auto_reset, seed, env_offset, prior_cols ? 1 : 0,
+                            reinterpret_cast<unsigned long long*>(span_out), stream);
 }
 
 int rcbf_safe_step_cols(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step, uint32_t* episode,
@@ -325,14 +369,18 @@ int rcbf_safe_step_cols(const rcbf_params* prm, int64_t B, double* x, double* au
                         int64_t env_offset, hipStream_t stream) {
     if (prm && prm->mode == RCBF_MODE_SIMULATED_CARS && mu_cols) return RCBF_E_BAD_SHAPE;  // the cars rows read no mean
     return safe_step_launch(prm, B, x, aux, step, episode, u_rl, mu_cols, sigma_cols, obs_out, u_out, reward, cost,
-                            done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset, 1, stream);
+                            done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset, 1, nullptr, stream);
 }
 
-int rcbf_safe_step_seq(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux, int32_t* step,
-                       uint32_t* episode, const float* const* u_rl_seq, int32_t n_u_rl, const float* mu,
-                       const float* sigma, float* obs_out, float* u_out, float* reward, float* cost, uint8_t* done,
-                       uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag, int32_t auto_reset, uint64_t seed,
-                       int64_t env_offset, hipStream_t stream) {
+}  // extern "C"
+
+namespace {
+
+int safe_step_seq_launch(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux, int32_t* step,
+                         uint32_t* episode, const float* const* u_rl_seq, int32_t n_u_rl, const float* mu,
+                         const float* sigma, int cols, float* obs_out, float* u_out, float* reward, float* cost,
+                         uint8_t* done, uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag,
+                         int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream) {
     if (int e = check_prm(prm)) return e;
     if (B < 0 || K < 0 || n_u_rl < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0 || K == 0) return 0;
@@ -341,15 +389,40 @@ int rcbf_safe_step_seq(const rcbf_params* prm, int64_t B, int32_t K, double* x, 
         if (!u_rl_seq[j]) return RCBF_E_NULL;
     if (!x || !aux || !step || !obs_out || !u_out || !reward || !cost || !done) return RCBF_E_NULL;
     if ((((uintptr_t)obs_out) & 7) || (((uintptr_t)x) & 15)) return RCBF_E_BAD_SHAPE;
+    if (cols && prm->mode == RCBF_MODE_SIMULATED_CARS && mu) return RCBF_E_BAD_SHAPE;  // the cars rows read no mean
     RCBF_DISPATCH(prm, {
         for (int32_t j = 0; j < K; ++j) {
-            hipLaunchKernelGGL((k_safe_step<SOLVER_, MODE_, K_>), dim3(grid_for_envs(B)), dim3(kBlock), 0, stream,
-                               B, x, aux, step, u_rl_seq[j % n_u_rl], episode, mu, sigma, obs_out, u_out, reward,
-                               cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset, *prm, 0);
+            launch_k_safe_step<SOLVER_, MODE_, K_>(B, x, aux, step, u_rl_seq[j % n_u_rl], episode, mu, sigma, obs_out,
+                                                   u_out, reward, cost, done, goal_met, status_out, fail_flag,
+                                                   auto_reset, seed, env_offset, *prm, cols, nullptr, stream);
             if (int e = launch_status()) return e;
         }
     });
     return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rcbf_safe_step_seq(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux, int32_t* step,
+                       uint32_t* episode, const float* const* u_rl_seq, int32_t n_u_rl, const float* mu,
+                       const float* sigma, float* obs_out, float* u_out, float* reward, float* cost, uint8_t* done,
+                       uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag, int32_t auto_reset, uint64_t seed,
+                       int64_t env_offset, hipStream_t stream) {
+    return safe_step_seq_launch(prm, B, K, x, aux, step, episode, u_rl_seq, n_u_rl, mu, sigma, 0, obs_out, u_out,
+                                reward, cost, done, goal_met, status_out, fail_flag, auto_reset, seed, env_offset,
+                                stream);
+}
+
+int rcbf_safe_step_seq_cols(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux, int32_t* step,
+                            uint32_t* episode, const float* const* u_rl_seq, int32_t n_u_rl, const float* mu_cols,
+                            const float* sigma_cols, float* obs_out, float* u_out, float* reward, float* cost,
+                            uint8_t* done, uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag,
+                            int32_t auto_reset, uint64_t seed, int64_t env_offset, hipStream_t stream) {
+    return safe_step_seq_launch(prm, B, K, x, aux, step, episode, u_rl_seq, n_u_rl, mu_cols, sigma_cols, 1, obs_out,
+                                u_out, reward, cost, done, goal_met, status_out, fail_flag, auto_reset, seed,
+                                env_offset, stream);
 }
 
 int rcbf_safe_rollout(const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux, int32_t* step,

@@ -113,13 +113,13 @@ __device__ __forceinline__ void load_layer_inputs(int64_t i, const float* x, con
     for (int c = 0; c < D::NU; ++c) us[c] = u[i * D::NU + c];
 }
 
-template <int SOLVER, int MODE, int K, bool FROM_OBS = false>
-__global__ void __launch_bounds__(kBlock) k_safe_action(rcbf_params prm, int64_t B, const float* __restrict__ x,
+template <int SOLVER, int MODE, int K, bool FROM_OBS = false, int BS = kBlock>
+__global__ void __launch_bounds__(BS) k_safe_action(rcbf_params prm, int64_t B, const float* __restrict__ x,
                                                         const float* __restrict__ u, const float* __restrict__ mu,
                                                         const float* __restrict__ sigma, float* __restrict__ u_out,
                                                         int32_t* __restrict__ status_out, int32_t* fail_flag) {
     using D = Dims<MODE, K>;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    int64_t i = env_index<BS>();
     if (i >= B) return;
     float xs[D::NS], us[D::NU], m[D::NS], s[D::NS], uf[D::NU];
     load_layer_inputs<MODE, K, FROM_OBS>(i, x, u, mu, sigma, xs, us, m, s);
@@ -137,15 +137,15 @@ __global__ void __launch_bounds__(kBlock) k_safe_action(rcbf_params prm, int64_t
 // backward passes where lo <= v <= hi).  dh_r/du_c is closed form:
 //   CBF rows: dh/du = Lg (cars) or a_j (unicycle) = -G_raw[r][c];
 //   actuator rows (u_max - u, -u_min + u): -1 / +1.
-template <int SOLVER, int MODE, int K, bool FROM_OBS = false>
-__global__ void __launch_bounds__(kBlock) k_safe_action_bwd(rcbf_params prm, int64_t B, const float* __restrict__ x,
+template <int SOLVER, int MODE, int K, bool FROM_OBS = false, int BS = kBlock>
+__global__ void __launch_bounds__(BS) k_safe_action_bwd(rcbf_params prm, int64_t B, const float* __restrict__ x,
                                                             const float* __restrict__ u, const float* __restrict__ mu,
                                                             const float* __restrict__ sigma,
                                                             const float* __restrict__ grad_u,
                                                             float* __restrict__ grad_u_rl) {
     using D = Dims<MODE, K>;
     constexpr int N = D::N, M = D::M, NU = D::NU;
-    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    int64_t i = env_index<BS>();
     if (i >= B) return;
     float xs[D::NS], us[NU], m[D::NS], s[D::NS], uf[NU];
     load_layer_inputs<MODE, K, FROM_OBS>(i, x, u, mu, sigma, xs, us, m, s);
@@ -305,8 +305,8 @@ int rcbf_safe_action(const rcbf_params* prm, int64_t B, const float* x, const fl
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !u_rl || !u_out) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_action<SOLVER_, MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0,
-                                          stream, *prm, B, x, u_rl, mu, sigma, u_out, status_out, fail_flag));
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action<SOLVER_, MODE_, K_, false, BS_>), stream, *prm, B, x, u_rl, mu,
+                                      sigma, u_out, status_out, fail_flag));
     return launch_status();
 }
 
@@ -317,8 +317,8 @@ int rcbf_safe_action_backward(const rcbf_params* prm, int64_t B, const float* x,
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !u_rl || !grad_u || !grad_u_rl) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_action_bwd<SOLVER_, MODE_, K_>), dim3(grid_for(B)), dim3(kBlock),
-                                          0, stream, *prm, B, x, u_rl, mu, sigma, grad_u, grad_u_rl));
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action_bwd<SOLVER_, MODE_, K_, false, BS_>), stream, *prm, B, x, u_rl,
+                                      mu, sigma, grad_u, grad_u_rl));
     return launch_status();
 }
 
@@ -329,8 +329,8 @@ int rcbf_obs_safe_action(const rcbf_params* prm, int64_t B, const float* obs, co
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!obs || !u_rl || !u_out) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_action<SOLVER_, MODE_, K_, true>), dim3(grid_for(B)), dim3(kBlock),
-                                          0, stream, *prm, B, obs, u_rl, mu, sigma, u_out, status_out, fail_flag));
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs, u_rl, mu,
+                                      sigma, u_out, status_out, fail_flag));
     return launch_status();
 }
 
@@ -341,8 +341,8 @@ int rcbf_obs_safe_action_backward(const rcbf_params* prm, int64_t B, const float
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!obs || !u_rl || !grad_u || !grad_u_rl) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_safe_action_bwd<SOLVER_, MODE_, K_, true>), dim3(grid_for(B)),
-                                          dim3(kBlock), 0, stream, *prm, B, obs, u_rl, mu, sigma, grad_u, grad_u_rl));
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action_bwd<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs,
+                                      u_rl, mu, sigma, grad_u, grad_u_rl));
     return launch_status();
 }
 

@@ -153,11 +153,16 @@ __device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_
 // The fused safe step (rcbf_safe_step): one env per lane.  ST = true only in
 // the study build (csrc/study/rcbf_stamps.hip), which records phase
 // timestamps into `stamps`; the product instantiation ignores it.
+// BS: workgroup size (block_for_envs).  SPAN = true (rcbf_safe_step_span, a
+// measurement entry point of the product library): lane 0 of every wave
+// writes the chip clock (s_memrealtime, 100 MHz) at its start and after its
+// own stores have completed to stamp_buf[2 w], [2 w + 1]; every other
+// instruction is the product's.
 // Argument order: B and the pointers of the first loads lead (one 64-B line
 // of the argument block, which the launch can preload into SGPRs), the
 // parameter block comes last.
-template <int SOLVER, int MODE, int K, bool ST = false>
-__global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restrict__ x, double* __restrict__ aux,
+template <int SOLVER, int MODE, int K, bool ST = false, int BS = kBlock, bool SPAN = false>
+__global__ void __launch_bounds__(BS) k_safe_step(int64_t B, double* __restrict__ x, double* __restrict__ aux,
                                                       int32_t* __restrict__ step, const float* __restrict__ u_rl,
                                                       uint32_t* __restrict__ episode, const float* __restrict__ mu,
                                                       const float* __restrict__ sigma, float* __restrict__ obs_out,
@@ -168,8 +173,10 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
                                                       int auto_reset, uint64_t seed, int64_t off, rcbf_params prm,
                                                       int prior_cols = 0, unsigned long long* stamp_buf = nullptr) {
     using D = Dims<MODE, K>;
-    int64_t i = env_index();
+    int64_t i = env_index<BS>();
     if (i >= B) return;
+    unsigned long long span_t0 = 0;
+    if constexpr (SPAN) span_t0 = __builtin_amdgcn_s_memrealtime();
     Stamps<ST> stamps;
     stamps.buf = stamp_buf;
     stamps.mark(0, false);
@@ -283,7 +290,7 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
         st_out(&aux[i], a);
         st_out(&step[i], st);
     }
-    __shared__ float obs_stage[kBlock / 64][64 * D::NO];
+    __shared__ float obs_stage[BS / 64][64 * D::NO];
     store_obs32_staged<MODE>(obs_out, i, B, xs, oc, obs_stage[threadIdx.x >> 6]);
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
@@ -294,6 +301,15 @@ __global__ void __launch_bounds__(kBlock) k_safe_step(int64_t B, double* __restr
     stamps.mark(6, false);
     report(status, status_out, i, fail_flag);
     stamps.mark(7, true);
+    if constexpr (SPAN) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have landed
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0) {
+            const int64_t w = ((int64_t)blockIdx.x * BS + threadIdx.x) >> 6;
+            typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<u2*>(stamp_buf + 2 * w) = u2{span_t0, t1};
+        }
+    }
 }
 
 }  // namespace rcbf

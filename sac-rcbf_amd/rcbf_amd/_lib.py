@@ -23,7 +23,7 @@ SOLVER_PDIPM = 1
 SOLVER_GI = 2
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NONFINITE = 0, 1, 2, 3
 MAX_HAZARDS = 8
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL"}
 
@@ -96,6 +96,10 @@ SIGNATURES = {
     "rcbf_safe_rollout": [_PRM, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _P],
     "rcbf_safe_step_seq": [_PRM, _I64, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                            _I32, _U64, _I64, _P],
+    "rcbf_safe_step_seq_cols": [_PRM, _I64, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                _I32, _U64, _I64, _P],
+    "rcbf_safe_step_span": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _U64,
+                            _I64, _P, _P],
     "rcbf_env_step_sync": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _I32, _U64, _I64, _P],
     "rcbf_host_alloc": [_I64, ctypes.POINTER(ctypes.c_void_p)],
     "rcbf_host_free": [_P],

@@ -144,6 +144,22 @@ class _QP(torch.autograd.Function):
         return None, None, gP, gq, gG, gh
 
 
+def _divide_rows_in_place(Gs, hs):
+    """The caller-visible side effect of the reference's solve_qp
+    (diff_cbf_qp.py:103-105): Gs divided in place by max |[G h]| of its row,
+    with torch's own division, so the caller sees the very rows qpth saw.
+    With autograd recording, the reference's own ops: the division and its
+    norm are differentiated (a leaf that requires grad raises torch's
+    in-place RuntimeError, as the reference does)."""
+    if torch.is_grad_enabled() and (Gs.requires_grad or hs.requires_grad):
+        Ghs = torch.cat((Gs, hs.to(Gs.dtype).unsqueeze(2)), -1)
+        Gs /= torch.max(torch.abs(Ghs), dim=2, keepdim=True)[0]
+    else:
+        with torch.no_grad():
+            Ghs = torch.cat((Gs, hs.to(Gs.dtype).unsqueeze(2)), -1)
+            Gs.div_(torch.max(torch.abs(Ghs), dim=2, keepdim=True)[0])
+
+
 class CBFQPLayer:
 
     def __init__(self, env, args, gamma_b=100, k_d=1.5, l_p=0.03, solver=_lib.SOLVER_ACTIVE_SET):
@@ -169,18 +185,18 @@ class CBFQPLayer:
         _lib.load()
 
     # -- diff_cbf_qp.py:44-79 ----------------------------------------------
-    def get_safe_action(self, state_batch, action_batch, mean_pred_batch, sigma_pred_batch):
+    def get_safe_action(self, state_batch, action_batch, mean_pred_batch, sigma_batch):
         expand_dims = len(state_batch.shape) == 1
         if expand_dims:
             action_batch = action_batch.unsqueeze(0)
             state_batch = state_batch.unsqueeze(0)
             mean_pred_batch = mean_pred_batch.unsqueeze(0) if mean_pred_batch is not None else None
-            sigma_pred_batch = sigma_pred_batch.unsqueeze(0) if sigma_pred_batch is not None else None
+            sigma_batch = sigma_batch.unsqueeze(0) if sigma_batch is not None else None
         out_device = action_batch.device if torch.is_tensor(action_batch) else self.device
         dev = _dev()
         x = _f32(state_batch, dev)
         mu = _f32(mean_pred_batch, dev) if mean_pred_batch is not None else None
-        sig = _f32(sigma_pred_batch, dev) if sigma_pred_batch is not None else None
+        sig = _f32(sigma_batch, dev) if sigma_batch is not None else None
         if torch.is_tensor(action_batch) and action_batch.requires_grad:
             u = action_batch.to(device=dev, dtype=torch.float32)
             if not u.is_contiguous():
@@ -225,8 +241,19 @@ class CBFQPLayer:
 
     # -- diff_cbf_qp.py:81-109 ---------------------------------------------
     def solve_qp(self, Ps, qs, Gs, hs):
-        """Row-normalise then solve; returns the solution without the slack."""
-        sol = self._qp(Ps, qs, Gs, hs, normalize=True)
+        """Row-normalise then solve; returns the solution without the slack.
+        The kernel normalises and solves in one launch (rcbf_qp_solve_saved,
+        normalize=1).  Like the reference (`Gs /= Ghs_norm`,
+        diff_cbf_qp.py:103-105) the caller's Gs tensor is divided in place:
+        without autograd history under no_grad, otherwise as the reference's
+        own in-place op (a leaf that requires grad raises the same
+        RuntimeError, a non-leaf records the division).  The solve reads a
+        copy of the rows, so the inputs its backward saved are not the ones
+        divided afterwards."""
+        G_in = Gs.clone() if torch.is_tensor(Gs) else Gs
+        sol = self._qp(Ps, qs, G_in, hs, normalize=True)
+        if torch.is_tensor(Gs) and torch.is_tensor(hs):
+            _divide_rows_in_place(Gs, hs)
         return sol[:, :-1]
 
     # -- diff_cbf_qp.py:111-144 --------------------------------------------

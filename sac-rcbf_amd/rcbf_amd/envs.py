@@ -284,10 +284,12 @@ class BatchedEnv:
         _lib.check(rc, "rcbf_safe_step")
         return self.obs, o["reward"], o["done"], o
 
-    def safe_step_seq(self, u_rl_seq, layer, mean=None, sigma=None, auto_reset=True, outputs=None, steps=None):
+    def safe_step_seq(self, u_rl_seq, layer, mean=None, sigma=None, auto_reset=True, outputs=None, steps=None,
+                      prior_layout="rows"):
         """`steps` fused safe steps (default len(u_rl_seq)) issued from ONE host
-        call (rcbf_safe_step_seq): step j uses u_rl_seq[j % len(u_rl_seq)],
-        each (B, n_u) f32 on this device.  Every step is its own launch of the
+        call (rcbf_safe_step_seq, or rcbf_safe_step_seq_cols for
+        prior_layout="cols"): step j uses u_rl_seq[j % len(u_rl_seq)], each
+        (B, n_u) f32 on this device.  Every step is its own launch of the
         fused kernel, exactly as `steps` calls of safe_step; the outputs hold
         the last step's values."""
         o = outputs if outputs is not None else self.make_outputs()
@@ -295,12 +297,29 @@ class BatchedEnv:
         if not us:
             raise ValueError("u_rl_seq is empty")
         K = len(us) if steps is None else int(steps)
-        mean, sigma = self._prior_arg(mean, "mean"), self._prior_arg(sigma, "sigma")
+        if prior_layout not in ("rows", "cols"):
+            raise ValueError(f"prior_layout must be 'rows' or 'cols', got {prior_layout!r}")
+        cols = prior_layout == "cols"
+        if cols:
+            if mean is not None and self.dynamics_mode == "SimulatedCars":
+                raise ValueError("the cars CBF rows read no mean (diff_cbf_qp.py:298-299): pass mean=None")
+            mean, sigma = self._prior_cols_arg(mean, "mean"), self._prior_cols_arg(sigma, "sigma")
+        else:
+            mean, sigma = self._prior_arg(mean, "mean"), self._prior_arg(sigma, "sigma")
         a = list(self._step_args(layer, o, auto_reset))
         stream = torch._C._cuda_getCurrentRawStream(self.device.index)
         ptrs = [t.data_ptr() for t in us]
-        fast = _fast_binding()
+        fast = None if cols else _fast_binding()
         tail = a[9:17] + a[17:20]
+        if cols:
+            arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+            rc = _lib.load().rcbf_safe_step_seq_cols(ctypes.byref(layer._prm), self.num_envs, K,
+                                                     *[v or None for v in a[2:6]], arr, len(ptrs),
+                                                     None if mean is None else mean.data_ptr(),
+                                                     None if sigma is None else sigma.data_ptr(),
+                                                     *[v or None for v in a[9:17]], *a[17:20], stream or None)
+            _lib.check(rc, "rcbf_safe_step_seq_cols")
+            return self.obs, o["reward"], o["done"], o
         if fast is not None:
             rc = fast.safe_step_seq(a[0], a[1], K, *a[2:6], ptrs, 0 if mean is None else mean.data_ptr(),
                                     0 if sigma is None else sigma.data_ptr(), *tail, stream)
@@ -312,6 +331,31 @@ class BatchedEnv:
                                                 None if sigma is None else sigma.data_ptr(),
                                                 *[v or None for v in a[9:17]], *a[17:20], stream or None)
         _lib.check(rc, "rcbf_safe_step_seq")
+        return self.obs, o["reward"], o["done"], o
+
+    def safe_step_span(self, u_rl, layer, span, mean=None, sigma=None, auto_reset=True, outputs=None,
+                       prior_layout="rows"):
+        """safe_step through the measurement entry point rcbf_safe_step_span:
+        the same step, plus each wave's start / end chip-clock stamps in
+        `span` ((ceil(B / 64), 2) int64 on this device).  bench.py only."""
+        o = outputs if outputs is not None else self.make_outputs()
+        u = self._u_arg(u_rl)
+        cols = prior_layout == "cols"
+        if cols:
+            mean, sigma = self._prior_cols_arg(mean, "mean"), self._prior_cols_arg(sigma, "sigma")
+        else:
+            mean, sigma = self._prior_arg(mean, "mean"), self._prior_arg(sigma, "sigma")
+        nw = (self.num_envs + 63) // 64
+        if not (torch.is_tensor(span) and span.dtype == torch.int64 and span.device == self.device
+                and span.is_contiguous() and span.numel() >= 2 * nw):
+            raise ValueError(f"span must be a contiguous int64 tensor of >= {2 * nw} entries on {self.device}")
+        a = self._step_args(layer, o, auto_reset)
+        rc = _lib.load().rcbf_safe_step_span(
+            ctypes.byref(layer._prm), self.num_envs, *[v or None for v in a[2:6]], u.data_ptr(),
+            None if mean is None else mean.data_ptr(), None if sigma is None else sigma.data_ptr(), int(cols),
+            *[v or None for v in a[9:17]], *a[17:20], span.data_ptr(),
+            torch._C._cuda_getCurrentRawStream(self.device.index) or None)
+        _lib.check(rc, "rcbf_safe_step_span")
         return self.obs, o["reward"], o["done"], o
 
     def _u_arg(self, u_rl):

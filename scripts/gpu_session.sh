@@ -31,18 +31,30 @@ wl_args() {  # bench.py arguments of a workload
     carsT) echo "--env SimulatedCars --prior tensor" ;;
     carsR) echo "--env SimulatedCars --prior rows" ;;
     uni5T) echo "--env Unicycle --hazards 5 --prior tensor" ;;
+    c1) echo "--config 1" ;;
+    c2) echo "--config 2" ;;
+    c3) echo "--config 3" ;;
+    c4) echo "--config 4" ;;
+    c4s) echo "--env SimulatedCars --batch 32768" ;;  # config 4's per-GPU shard at 8 GPUs
+    c5) echo "--config 5" ;;
   esac
 }
-wl_kernel() {  # the fused kernel's name in rocprofv3 output
+wl_kernel() {  # the timed kernel's name in rocprofv3 output (workgroup size from rcbf_common.hpp block_for_envs)
   case $1 in
-    cars|carsT|carsR) echo 'k_safe_step<0, 0, 1, false>' ;;
-    uni3) echo 'k_safe_step<0, 1, 3, false>' ;;
-    uni5|uni5T) echo 'k_safe_step<0, 1, 5, false>' ;;
+    cars|carsT|carsR|c4) echo 'k_safe_step<0, 0, 1, false, 256, false>' ;;
+    uni3) echo 'k_safe_step<0, 1, 3, false, 256, false>' ;;
+    uni5|uni5T) echo 'k_safe_step<0, 1, 5, false, 256, false>' ;;
+    c1|c2) echo 'k_safe_step<0, 0, 1, false, 64, false>' ;;
+    c3) echo 'k_safe_step<0, 1, 3, false, 64, false>' ;;
+    c4s) echo 'k_safe_step<0, 0, 1, false, 128, false>' ;;
+    c5) echo 'k_safe_action<0, 0, 1, true, 64>' ;;
   esac
 }
-wl_name() {
-  case $1 in cars) echo cars ;; uni3) echo unicycle3 ;; uni5) echo unicycle5 ;;
-    carsT) echo cars_tensorprior ;; carsR) echo cars_rowsprior ;; uni5T) echo unicycle5_tensorprior ;; esac
+wl_name() {  # <short>_B<batch>, the workload's name in profiles/ (bench.py workload_short)
+  case $1 in cars) echo cars_B65536 ;; uni3) echo uni3_B65536 ;; uni5) echo uni5_B65536 ;;
+    carsT) echo cars_tensorprior_B65536 ;; carsR) echo cars_rowsprior_B65536 ;; uni5T) echo uni5_tensorprior_B65536 ;;
+    c1) echo cars_B1 ;; c2) echo cars_B4096 ;; c3) echo uni3_B4096 ;; c4) echo cars_B262144 ;; c4s) echo cars_B32768 ;;
+    c5) echo sacupd_cars_B4096 ;; esac
 }
 for step in "$@"; do
   wl=${step#*_}
@@ -57,16 +69,19 @@ for step in "$@"; do
         run "sweep_${w}_$b" 300 python bench.py --no-cpu-baseline --batch "$b" $(wl_args "$w")
       done; done ;;
     b_*)    run "b_$wl" 300 python bench.py --no-cpu-baseline $(wl_args "$wl") ;;
+    bc_*)   run "bc_$wl" 400 python bench.py $(wl_args "$wl") ;;  # with the CPU baselines
     prof_*)
       run "prof_$wl" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$wl" -o run -- \
         python3 bench.py --no-cpu-baseline $(wl_args "$wl")
       [ -f "$OUT/prof_$wl/run_kernel_trace.csv" ] && python scripts/trace_summary.py "$OUT/prof_$wl/run_kernel_trace.csv" \
-        "$(wl_kernel "$wl")" "$OUT/$(wl_name "$wl")_B65536_kernel_trace_summary.json" ;;
+        "$(wl_kernel "$wl")" "$OUT/$(wl_name "$wl")_kernel_trace_summary.json"
+      [ -f "$OUT/prof_$wl/run_kernel_stats.csv" ] && cp "$OUT/prof_$wl/run_kernel_stats.csv" "$OUT/kernel_stats_$(wl_name "$wl")_$TAG.csv" ;;
     profdrv)  # the driver's own command under the tracer
       run profdrv 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profdrv" -o run -- \
         python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
       [ -f "$OUT/profdrv/run_kernel_trace.csv" ] && python scripts/trace_summary.py "$OUT/profdrv/run_kernel_trace.csv" \
-        "$(wl_kernel cars)" "$OUT/cars_B65536_driver_form_kernel_trace_summary.json" ;;
+        "$(wl_kernel cars)" "$OUT/cars_B65536_driver_form_kernel_trace_summary.json"
+      [ -f "$OUT/profdrv/run_kernel_stats.csv" ] && cp "$OUT/profdrv/run_kernel_stats.csv" "$OUT/kernel_stats_driver_form_cars_$TAG.csv" ;;
     pmc_*)
       run "pmcf_$wl" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcf_$wl" -o run -- \
         python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 $(wl_args "$wl")
@@ -74,13 +89,20 @@ for step in "$@"; do
         python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 $(wl_args "$wl")
       if [ -f "$OUT/pmcf_$wl/run_counter_collection.csv" ] && [ -f "$OUT/pmcw_$wl/run_counter_collection.csv" ]; then
         python scripts/pmc_traffic.py "$OUT/pmcf_$wl/run_counter_collection.csv" "$OUT/pmcw_$wl/run_counter_collection.csv" \
-          "$(wl_kernel "$wl")" "$OUT/pmc_traffic_$(wl_name "$wl")_B65536.json" B=65536 workload="$(wl_name "$wl")" > /dev/null
+          "$(wl_kernel "$wl")" "$OUT/pmc_traffic_$(wl_name "$wl").json" workload="$(wl_name "$wl")" > /dev/null
       fi ;;
     sq_*)
       run "sq_$wl" 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
         --output-format csv -d "$OUT/sq_$wl" -o run -- python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 $(wl_args "$wl")
       [ -f "$OUT/sq_$wl/run_counter_collection.csv" ] && python scripts/pmc_sq.py "$OUT/sq_$wl/run_counter_collection.csv" \
-        "$(wl_kernel "$wl")" > "$OUT/pmc_sq_$(wl_name "$wl")_B65536.txt" ;;
+        "$(wl_kernel "$wl")" > "$OUT/pmc_sq_$(wl_name "$wl").txt" ;;
+    tracer)  # control: torch kernels of the same bytes, untraced (events) and traced
+      run tracer_plain 120 python scripts/tracer_control.py
+      run tracer_traced 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/tracer" -o run -- \
+        python3 scripts/tracer_control.py
+      [ -f "$OUT/tracer/run_kernel_stats.csv" ] && cp "$OUT/tracer/run_kernel_stats.csv" "$OUT/kernel_stats_tracer_control_$TAG.csv" ;;
+    abbs)  bash scripts/ab_multi.sh "$TAG/abbs" "bs256" c2 c3 c4s c5 || exit 1 ;;
+    absin) bash scripts/ab_multi.sh "$TAG/absin" "nosincos" u5 u3 || exit 1 ;;
     *) log "unknown step $step" ;;
   esac
 done

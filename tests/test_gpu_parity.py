@@ -139,6 +139,54 @@ def test_solve_qp_and_cbf_layer_surface(golden):
     assert rel(z, d["prior_z"]) <= 1e-6
 
 
+def test_layer_surfaces_by_keyword(golden):
+    """Every layer surface called with the reference's keyword names
+    (diff_cbf_qp.py:12,44,81,111,146; cbf_qp.py:7,29,55,242) gives the
+    positional result, and solve_qp divides the caller's Gs in place like
+    `Gs /= Ghs_norm` (diff_cbf_qp.py:105): bit for bit the reference's rows."""
+    from rcbf_amd.cbf_qp import CascadeCBFLayer
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import SimulatedCarsEnv
+    d = golden("cars_layer")
+    layer = CBFQPLayer(env=_env("SimulatedCars"), args=Args(), gamma_b=float(d["gamma_b"]), k_d=1.5, l_p=0.03)
+    x, u, mu, sg = (dev(d["rand" + k]) for k in ("_x", "_u", "_mu", "_sigma"))
+    fin = layer.get_safe_action(state_batch=x, action_batch=u, mean_pred_batch=mu, sigma_batch=sg)
+    assert torch.equal(fin, layer.get_safe_action(x, u, mu, sg))
+    assert rel(fin.cpu().numpy(), d["rand_final"]) <= 1e-5
+    P, q, G, h = layer.get_cbf_qp_constraints(state_batch=x, action_batch=u, mean_pred_batch=mu,
+                                              sigma_pred_batch=sg)
+    assert np.array_equal(G.cpu().numpy(), d["rand_G"])
+    Gpos = G.clone()
+    sol_pos = layer.solve_qp(P, q, Gpos, h)
+    sol = layer.solve_qp(Ps=P, qs=q, Gs=G, hs=h)
+    assert torch.equal(sol, sol_pos)
+    assert np.array_equal(G.cpu().numpy(), d["rand_Gn"]) and torch.equal(G, Gpos)  # divided in place
+    z = layer.cbf_layer(Qs=P, ps=q, Gs=dev(d["rand_Gn"]), hs=dev(d["rand_hn"]), As=None, bs=None,
+                        solver_args={"eps": 1e-4})
+    assert rel(z.cpu().numpy(), d["rand_z"]) <= 1e-6
+    # autograd: a leaf that requires grad refuses the in-place division, as in the reference
+    Gl = dev(d["rand_G"]).requires_grad_(True)
+    with pytest.raises(RuntimeError):
+        layer.solve_qp(P, q, Gl, h)
+    # a non-leaf is divided with the division recorded; d sol / d G flows to the leaf
+    G0 = dev(d["rand_G"]).requires_grad_(True)
+    Gn = G0 * 1.0
+    s2 = layer.solve_qp(P, q, Gn, h)
+    assert torch.equal(Gn.detach(), dev(d["rand_Gn"])) and rel(s2.detach().cpu().numpy(), d["rand_z"][:, :1]) <= 1e-6
+    s2.sum().backward()
+    assert G0.grad is not None and torch.isfinite(G0.grad).all()
+    # Cascade surfaces by keyword
+    c = golden("cascade")
+    cl = CascadeCBFLayer(env=SimulatedCarsEnv(), gamma_b=20.0, k_d=3.0, l_p=0.03)
+    us = cl.get_u_safe(u_nom=c["cars_u"], s=c["cars_x"], mean_pred=c["cars_mu"], sigma=c["cars_sigma"])
+    assert np.array_equal(np.asarray(us), np.asarray(cl.get_u_safe(c["cars_u"], c["cars_x"], c["cars_mu"],
+                                                                   c["cars_sigma"])))
+    Pc, qc, Gc, hc = cl.get_cbf_qp_constraints(u_nom=c["cars_u"][0], state=c["cars_x"][0],
+                                              mean_pred=c["cars_mu"][0], sigma_pred=c["cars_sigma"][0])
+    uc = cl.solve_qp(P=Pc, q=qc, G=np.array(Gc, copy=True), h=hc)
+    assert rel(uc, cl.solve_qp(Pc, qc, np.array(Gc, copy=True), hc)) == 0.0
+
+
 def test_single_sample_and_empty_batch(golden):
     d = golden("cars_layer")
     layer = _layer(_env("SimulatedCars"), float(d["gamma_b"]))

@@ -93,7 +93,9 @@ def test_solve_qp_and_cbf_layer_autograd(normalize):
     layer = _layer()
     Pt, qt, Gt, ht = (dev(a).requires_grad_(True) for a in (P, q, G, h))
     if normalize:
-        out = layer.solve_qp(Pt, qt, Gt, ht)
+        # solve_qp divides the caller's Gs in place (diff_cbf_qp.py:105), so like the reference's
+        # callers (whose Gs come out of get_cbf_qp_constraints) it takes a non-leaf G
+        out = layer.solve_qp(Pt, qt, Gt * 1.0, ht)
         assert out.shape == (B, n - 1)
         (out * dev(w[:, :n - 1])).sum().backward()
         w = np.concatenate([w[:, :n - 1], np.zeros((B, 1), np.float32)], axis=1)
@@ -124,7 +126,7 @@ def test_solve_qp_autograd_with_pdipm_layer(normalize):
     layer = CBFQPLayer(BatchedSimulatedCarsEnv(4), Args(), gamma_b=20.0, solver=_lib.SOLVER_PDIPM)
     Pt, qt, Gt, ht = (dev(a).requires_grad_(True) for a in (P, q, G, h))
     if normalize:
-        out = layer.solve_qp(Pt, qt, Gt, ht)
+        out = layer.solve_qp(Pt, qt, Gt * 1.0, ht)  # a non-leaf G: solve_qp divides it in place
         (out * dev(w[:, :n - 1])).sum().backward()
         w = np.concatenate([w[:, :n - 1], np.zeros((B, 1), np.float32)], axis=1)
     else:
