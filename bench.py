@@ -546,7 +546,7 @@ def main():
     kernels = dominant_kernels(args, B)
     k_us_rp, rp_src = rocprof_kernel_us(short, B, kernels)
     span = {}
-    if rank == 0 and not args.cpu_dry_run and not args.no_span and args.workload == "step":
+    if world == 1 and not args.cpu_dry_run and not args.no_span and args.workload == "step":
         span = measure_span(env, layer, ctx, dev, B, bps)
     extra = {}
     if args.extra and rank == 0 and not args.cpu_dry_run and args.workload == "step":

@@ -208,6 +208,30 @@ struct LayerState {
 // without the row normalisation -- a positive scaling of each row that the
 // exact optimum does not depend on (cars_qp_1d_raw); L.G / L.h then hold the
 // raw rows and L.Nrm / L.ish are not set.
+// The exact solve of the RAW rows (the fused safe step's layer, after the
+// rows are built): P of the diff layer, the closed-form solver of the mode,
+// then u_final = clamp(u + z[:n_u]) (diff_cbf_qp.py:77).  Shared by
+// layer_forward<..., RAW> and the cars early-store order in k_safe_step.
+template <int MODE, int K>
+__device__ __forceinline__ void layer_solve_raw(const rcbf_params& prm, const float* u, float* u_final,
+                                                LayerState<MODE, K>& L) {
+    using D = Dims<MODE, K>;
+    PMat<D::N, true> pm;
+    double pd[D::N];
+    diff_P<MODE>(pd);
+    pmat_set_diag<D::N>(pm, pd);
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS)
+        cars_qp_1d_raw<float>(pm, L.G, L.h, L.qp.z, L.qp.status);
+    else
+        uni_qp_2d_raw<K, float>(pm, L.G, L.h, L.qp.z, L.qp.status);
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) {
+        float v = u[c] + (float)L.qp.z[c];
+        float lo = (float)prm.u_min[c], hi = (float)prm.u_max[c];
+        u_final[c] = fminf(fmaxf(v, lo), hi);  // torch.clamp (diff_cbf_qp.py:77)
+    }
+}
+
 template <int SOLVER, int MODE, int K, bool NEED_LAM = false, bool ST = false, bool RAW = false>
 __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const float* xs, const float* u,
                                               const float* mu, const float* sig, float* u_final,
@@ -217,21 +241,8 @@ __device__ __forceinline__ void layer_forward(const rcbf_params& prm, const floa
     diff_rows<MODE, K>(prm, xs, u, mu, sig, L.G, L.h, cs_row);
     if constexpr (RAW && SOLVER == RCBF_SOLVER_ACTIVE_SET && !NEED_LAM) {
         stamps.mark(3, false);
-        PMat<D::N, true> pm;
-        double pd[D::N];
-        diff_P<MODE>(pd);
-        pmat_set_diag<D::N>(pm, pd);
-        if constexpr (MODE == RCBF_MODE_SIMULATED_CARS)
-            cars_qp_1d_raw<float>(pm, L.G, L.h, L.qp.z, L.qp.status);
-        else
-            uni_qp_2d_raw<K, float>(pm, L.G, L.h, L.qp.z, L.qp.status);
+        layer_solve_raw<MODE, K>(prm, u, u_final, L);
         stamps.mark(4, false);
-#pragma unroll
-        for (int c = 0; c < D::NU; ++c) {
-            float v = u[c] + (float)L.qp.z[c];
-            float lo = (float)prm.u_min[c], hi = (float)prm.u_max[c];
-            u_final[c] = fminf(fmaxf(v, lo), hi);  // torch.clamp (diff_cbf_qp.py:77)
-        }
         return;
     }
 #pragma unroll

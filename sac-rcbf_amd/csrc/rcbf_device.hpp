@@ -1878,8 +1878,10 @@ struct CarsStepOut {
 // that does not depend on it (all positions, the velocities of cars 0, 1, 2
 // and 4, t, step, done, cost) and returns car 3's acceleration; cars_env_post
 // adds g u to car 3's velocity and forms the reward.  pre + post is exactly
-// the reference's step.  (Storing the pre part before the QP so its writes
-// overlap the QP measured no faster: profiles/r01/ablate_early_store.txt.)
+// the reference's step.  k_safe_step stores the state the pre part fixes
+// before the layer's chain runs (RCBF_EARLY_STORE, the product default since
+// r03: 3.85 -> 3.67 us per step, profiles/r03/early_store_confirm_r03k.txt;
+// r01's first form of it measured no faster, profiles/r01/ablate_early_store.txt).
 __device__ __forceinline__ double cars_env_pre(const rcbf_params& prm, double* xs, double& t, int& step,
                                                CarsStepOut& o) {
 #pragma clang fp contract(off)

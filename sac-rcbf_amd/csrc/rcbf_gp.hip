@@ -42,14 +42,21 @@ constexpr int kGpChunk = 256;  // training rows staged in LDS at a time
 // [s per, (s + 1) per); it stores its raw Q tile to
 // qraw[((i * n_split + s) * B + b) * C_pad + col] and k_gp_combine adds the
 // n_split tiles (fixed order, deterministic) before squaring.
-template <int D, int CT, bool SK = false>
-__global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
-                                                  float* __restrict__ partial, float* __restrict__ meanraw,
-                                                  int n_split = 1, float* __restrict__ qraw = nullptr) {
+// The mean column (logical column r) of the single pass is not taken from
+// the fp32 MFMA accumulator (one running sum over all N training rows: the
+// large alternating alpha of an ill-conditioned fit made that chain lose
+// 3e-4 of max|mean|).  Each lane instead adds its own A value times alpha_n
+// (staged in LDS with the chunk) into an fp64 sum -- the products of two
+// fp32 values are exact in fp64 -- and the two half-waves' sums are added in
+// the epilogue.  One v_fma_f64 per k-step beside four MFMAs.
+// MEAN: this workgroup's column block holds the mean column r (a separate
+// instantiation, so the other ~95 % of the workgroups run the plain loop).
+template <int D, int CT, bool SK, bool MEAN>
+__device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B, const float* __restrict__ xq,
+                                              float* __restrict__ partial, float* __restrict__ meanraw, int n_split,
+                                              float* __restrict__ qraw, float4* s_xt, float* s_tn, float* s_alpha) {
     constexpr int DP = (D + 3) / 4 * 4;  // LDS row stride (float4 reads)
     constexpr float kL2E = 1.4426950408889634f;
-    __shared__ float4 s_xt[kGpChunk * DP / 4];
-    __shared__ float s_tn[kGpChunk];
 
     // CT column tiles of 32 per wave: 4 (the whole 128-column block) or 2
     // (half of it, twice the workgroups for small query batches)
@@ -100,6 +107,16 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
         n_beg = min(m.N_pad, split * per);
         n_end = min(m.N_pad, n_beg + per);
     }
+    // does this workgroup hold the mean column r (uniform)?  alpha_n = Rt[n][r] sits at the physical
+    // column of logical column r (128-column blocks, lane-interleaved: 4 l + c holds 32 c + l)
+    const int r_rank = m.r;
+    const int mcol = r_rank - (cb * kGpCols + 32 * CT * sub);
+    constexpr bool has_mean = MEAN && !SK;
+    (void)mcol;
+    const int64_t alpha_phys = (int64_t)(r_rank / kGpCols) * kGpCols + 4 * ((r_rank % kGpCols) % 32) +
+                               (r_rank % kGpCols) / 32;
+    const float* alpha_i = m.Rt + (int64_t)i * m.N_pad * ldc + alpha_phys;
+    double macc = 0.0;
     for (int n0 = n_beg; n0 < n_end; n0 += kGpChunk) {
         const int nch = min(kGpChunk, n_end - n0);  // multiple of 32
         __syncthreads();
@@ -111,6 +128,9 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
             for (int q = 0; q < DP / 4; ++q)
                 s_xt[e * (DP / 4) + q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
             s_tn[e] = -kL2E * tn2_i[n0 + e];
+            if constexpr (!SK) {
+                if (has_mean) s_alpha[e] = alpha_i[(int64_t)(n0 + e) * ldc];
+            }
         }
         __syncthreads();
         // B operand of k-step kk: Rt[n0 + kk + half][cb*128 + 32c + l32]
@@ -151,6 +171,9 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
 #pragma unroll
                 for (int c = 0; c < CT; ++c)
                     acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bcur[q][c], acc[c], 0, 0, 0);
+                if constexpr (!SK) {
+                    if (has_mean) macc = fma((double)av, (double)s_alpha[nl], macc);
+                }
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -172,7 +195,6 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
         }
         return;
     }
-    const int r_rank = m.r;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int64_t row = b0 + 32 * w + (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -182,12 +204,31 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
             const int col = cb * kGpCols + 32 * (c + CT * sub) + l32;
             const float q = acc[c][r];
             v += (col < r_rank) ? q * q : 0.0f;
-            if (col == r_rank && row < B) meanraw[(int64_t)i * B + row] = q;
         }
 #pragma unroll
         for (int msk = 1; msk < 32; msk <<= 1) v += __shfl_xor(v, msk, 64);
         if (l32 == 0 && row < B) partial[((int64_t)i * n_part + blockIdx.y) * B + row] = v;
     }
+    if constexpr (has_mean) {  // lane (l32, half) summed row b0 + 32 w + l32 over the training rows of parity half
+        const double tot = macc + __shfl_xor(macc, 32, 64);
+        const int64_t row = b0 + 32 * w + l32;
+        if (half == 0 && row < B) meanraw[(int64_t)i * B + row] = (float)tot;
+    }
+}
+
+template <int D, int CT, bool SK = false>
+__global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
+                                                  float* __restrict__ partial, float* __restrict__ meanraw,
+                                                  int n_split = 1, float* __restrict__ qraw = nullptr) {
+    constexpr int DP = (D + 3) / 4 * 4;
+    __shared__ float4 s_xt[kGpChunk * DP / 4];
+    __shared__ float s_tn[kGpChunk];
+    __shared__ float s_alpha[SK ? 1 : kGpChunk];
+    const int mcol = m.r - ((int)(blockIdx.y / (4 / CT)) * kGpCols + 32 * CT * (int)(blockIdx.y % (4 / CT)));
+    if (!SK && mcol >= 0 && mcol < 32 * CT)  // uniform: the block holding the mean column
+        gp_qform_body<D, CT, SK, true>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha);
+    else
+        gp_qform_body<D, CT, SK, false>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha);
 }
 
 // Few queries (B <= 8): the posterior is a GEMV per GP, bound by streaming
@@ -334,28 +375,44 @@ struct GpCols {
     int32_t idx[10];
 };
 
-__global__ void __launch_bounds__(256) k_gp_finish(rcbf_gp_model m, int64_t B, int n_cb,
-                                                   const float* __restrict__ partial,
-                                                   const float* __restrict__ meanraw, float* __restrict__ mean_out,
-                                                   float* __restrict__ std_out, GpCols cols,
-                                                   float* __restrict__ mean_cols, float* __restrict__ std_cols) {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= B * m.n_s) return;
-    const int i = (int)(e % m.n_s);
-    const int64_t b = e / m.n_s;
+// mean and std of GP i at query b (dynamics.py:371-380 after gpytorch)
+__device__ __forceinline__ void gp_mean_std(const rcbf_gp_model& m, int64_t B, int n_cb, const float* partial,
+                                            const float* meanraw, int i, int64_t b, float& mu, float& sd) {
     float q = 0.0f;
     for (int c = 0; c < n_cb; ++c) q += partial[((int64_t)i * n_cb + c) * B + b];
     const float lat = fmaxf(m.outscale[i] - q, 0.0f);  // latent posterior variance
     const float var = lat + m.noise[i];                  // likelihood(model(x)).variance
-    const float mu = meanraw[(int64_t)i * B + b] * m.y_scale[i];
-    const float sd = sqrtf(var) * m.y_scale[i];
+    mu = meanraw[(int64_t)i * B + b] * m.y_scale[i];
+    sd = sqrtf(var) * m.y_scale[i];
+}
+
+// (B, n_s) row outputs, thread e = b n_s + i
+__global__ void __launch_bounds__(256) k_gp_finish(rcbf_gp_model m, int64_t B, int n_cb,
+                                                   const float* __restrict__ partial,
+                                                   const float* __restrict__ meanraw, float* __restrict__ mean_out,
+                                                   float* __restrict__ std_out) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= B * m.n_s) return;
+    float mu, sd;
+    gp_mean_std(m, B, n_cb, partial, meanraw, (int)(e % m.n_s), e / m.n_s, mu, sd);
     if (mean_out) mean_out[e] = mu;
     if (std_out) std_out[e] = sd;
-    for (int c = 0; c < cols.n; ++c) {
-        if (cols.idx[c] != i) continue;
-        if (mean_cols) mean_cols[(int64_t)c * B + b] = mu;
-        if (std_cols) std_cols[(int64_t)c * B + b] = sd;
-    }
+}
+
+// column outputs (cols.n, B), thread e = c B + b: consecutive lanes store
+// consecutive b of one column (the same arithmetic as k_gp_finish, so the
+// same values bit for bit)
+__global__ void __launch_bounds__(256) k_gp_finish_cols(rcbf_gp_model m, int64_t B, int n_cb,
+                                                        const float* __restrict__ partial,
+                                                        const float* __restrict__ meanraw, GpCols cols,
+                                                        float* __restrict__ mean_cols, float* __restrict__ std_cols) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= B * cols.n) return;
+    const int c = (int)(e / B);
+    float mu, sd;
+    gp_mean_std(m, B, n_cb, partial, meanraw, cols.idx[c], e % B, mu, sd);
+    if (mean_cols) mean_cols[e] = mu;
+    if (std_cols) std_cols[e] = sd;
 }
 
 // Split-K factor: 1 when the (query tile x column block x GP) grid already
@@ -479,9 +536,16 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
         hipLaunchKernelGGL(k_gp_combine, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, *m, B, n_cb, sk,
                            qraw, partial, meanraw);
     }
-    const int64_t tot = B * m->n_s;
-    hipLaunchKernelGGL(k_gp_finish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *m, B, n_part,
-                       partial, meanraw, mean_out, std_out, gc, mean_cols, std_cols);
+    if (mean_out || std_out) {
+        const int64_t tot = B * m->n_s;
+        hipLaunchKernelGGL(k_gp_finish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *m, B, n_part,
+                           partial, meanraw, mean_out, std_out);
+    }
+    if (gc.n > 0) {
+        const int64_t tot = B * gc.n;
+        hipLaunchKernelGGL(k_gp_finish_cols, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, *m, B,
+                           n_part, partial, meanraw, gc, mean_cols, std_cols);
+    }
     return launch_status();
 }
 

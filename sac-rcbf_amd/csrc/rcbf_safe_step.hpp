@@ -266,14 +266,7 @@ __global__ void __launch_bounds__(BS) k_safe_step(int64_t B, double* __restrict_
         st_out(&step[i], st);
         __builtin_amdgcn_sched_barrier(0);  // keep the early stores ahead of the layer's chain
         if constexpr (kRowsFirst) {
-            PMat<D::N, true> pm;
-            double pd[D::N];
-            diff_P<MODE>(pd);
-            pmat_set_diag<D::N>(pm, pd);
-            cars_qp_1d_raw<float>(pm, L.G, L.h, L.qp.z, L.qp.status);
-#pragma unroll
-            for (int c = 0; c < D::NU; ++c)  // torch.clamp (diff_cbf_qp.py:77)
-                uf[c] = fminf(fmaxf(us[c] + (float)L.qp.z[c], (float)prm.u_min[c]), (float)prm.u_max[c]);
+            layer_solve_raw<MODE, K>(prm, us, uf, L);  // the same solve as layer_forward<..., RAW>
         } else {
             layer_forward<SOLVER, MODE, K, false, false, RCBF_FUSED_RAW_ROWS != 0>(prm, s32, us, m, s, uf, L);
         }

@@ -101,6 +101,12 @@ for step in "$@"; do
       run tracer_traced 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/tracer" -o run -- \
         python3 scripts/tracer_control.py
       [ -f "$OUT/tracer/run_kernel_stats.csv" ] && cp "$OUT/tracer/run_kernel_stats.csv" "$OUT/kernel_stats_tracer_control_$TAG.csv" ;;
+    gpab)  # GP posterior timing, product vs build/variants/librcbf_gpold.so, 3 rounds (scripts/gp_bench.py, n_s 10, N 3000)
+      for r in 1 2 3; do for n in prod gpold; do
+        if [ "$n" = prod ]; then lib=""; else lib="RCBF_HIP_LIB=build/variants/librcbf_$n.so"; fi
+        env $lib timeout -k 10 200 python scripts/gp_bench.py 10 3000 > "$OUT/gp_${n}_$r.log" 2>&1 || exit 1
+        echo "$n $(tail -1 "$OUT/gp_${n}_$r.log")" >> "$OUT/gpab_sum.txt"
+      done; done ;;
     abbs)  bash scripts/ab_multi.sh "$TAG/abbs" "bs256" c2 c3 c4s c5 || exit 1 ;;
     absin) bash scripts/ab_multi.sh "$TAG/absin" "nosincos" u5 u3 || exit 1 ;;
     *) log "unknown step $step" ;;
