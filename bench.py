@@ -159,8 +159,13 @@ def cpu_sac_update(env_name, hazards, seconds, B):
     from oracle import oracle as O
     rng = np.random.default_rng(3)
     hz = O.UNI["hazards"][:hazards] if env_name == "Unicycle" else None
-    if env_name == "SimulatedCars":
-        x, _, _ = O.cars_reset(rng.normal(0, 0.5, B))
+    if env_name == "SimulatedCars":  # SURVEY 8(d) states: seeded resets advanced 0-299 steps under u ~ U[-1, 1]
+        x, t, st = O.cars_reset(rng.normal(0, 0.5, B))
+        stop = rng.integers(0, 300, B)
+        for k in range(int(stop.max())):
+            xn, tn, sn, _, _, _, _ = O.cars_step(x, t, st, rng.uniform(-1, 1, (B, 1)).astype(np.float32))
+            go = (k < stop)[:, None]
+            x, t, st = np.where(go, xn, x), np.where(go[:, 0], tn, t), np.where(go[:, 0], sn, st)
         obs = O.cars_obs(x).astype(np.float32)
         n_u = 1
     else:
@@ -572,6 +577,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f32 rows / f64 QP" if sac else "f32 rows / f64 QP / f64 env",
         "data": ("dry run: launcher and collectives only, no kernel, not a measurement" if args.cpu_dry_run else
+                 "synthetic (fp32 observations of SURVEY 8(d) states one env step on, policy actions ~ U[-1,1], "
+                 "upstream gradient ~ N(0,1), prior mean/sigma)" if sac else
                  "synthetic (SURVEY 8(d) start states, u_RL ~ U[-1,1], "
                  + {"prior": "prior mean/sigma",
                     "tensor": "per-env mean/sigma, column layout of rcbf_gp_predict_cols (post-GP-fit regime)",
@@ -725,6 +732,8 @@ def setup_sac_update(args, dev, rank, B):
     gen = torch.Generator(device=dev)
     gen.manual_seed(2000 + rank)
     init_states(env, gen, args.env)
+    # a replay batch: the observations of SURVEY 8(d) states one env step on (load_state leaves obs as it was)
+    env.step(torch.rand(B, env.n_u, device=dev, generator=gen) * 2 - 1, auto_reset=False)
     obs = env.obs.clone()
     S = largest_divisor_le(args.steps, args.graph_steps)
     npool = min(S, 50)
