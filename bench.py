@@ -87,6 +87,10 @@ def parse():
                     help="step: the fused safe step; sac_update: RCBF_SAC.get_safe_action on a replay batch "
                          "forward + backward (rcbf_obs_safe_action + its backward, config 5)")
     ap.add_argument("--no-span", action="store_true", help="skip the untimed in-kernel span measurement")
+    ap.add_argument("--sac-bwd", default="jac", choices=["jac", "resolve"],
+                    help="config 5's backward: jac = the forward keeps d final / d u (rcbf_obs_safe_action_jac) and "
+                         "the backward applies it (rcbf_safe_action_apply_jac), as the autograd op runs it; resolve "
+                         "= the plain forward and the re-solving backward (rcbf_obs_safe_action_backward)")
     args = ap.parse_args()
     preset = {1: dict(env="SimulatedCars", batch=1, workload="step"),
               2: dict(env="SimulatedCars", batch=4096, workload="step"),
@@ -342,11 +346,12 @@ METRICS = {
 }
 
 # Algorithmic bytes of one forward + backward of the SAC-update safe action
-# per row, prior mean/sigma (config 5): forward reads obs + u_RL, writes u;
-# backward reads obs + u_RL + grad_u, writes grad_u_RL.
-#   cars     fwd 40 + 4 + 4 = 48,  bwd 40 + 4 + 4 + 4 = 52  -> 100
-#   unicycle fwd 28 + 8 + 8 = 44,  bwd 28 + 8 + 8 + 8 = 52  ->  96
-SAC_UPDATE_BYTES = {"SimulatedCars": 100, "Unicycle": 96}
+# per row, prior mean/sigma (config 5): the op's own inputs and outputs --
+# obs + u_RL in, u out (forward), grad_u in, grad_u_RL out (backward):
+#   cars     40 + 4 + 4 + 4 + 4 = 56;   unicycle 28 + 8 + 8 + 8 + 8 = 60.
+# What an implementation keeps between the two (the saved Jacobian, 8 / 32 B,
+# or re-reading obs and u_RL) is traffic, not algorithmic bytes.
+SAC_UPDATE_BYTES = {"SimulatedCars": 56, "Unicycle": 60}
 
 
 def block_for_envs(B):
@@ -369,6 +374,8 @@ def dominant_kernels(args, B):
     mode, K = (0, 1) if args.env == "SimulatedCars" else (1, args.hazards)
     bs = block_for_envs(B)
     if args.workload == "sac_update":
+        if args.sac_bwd == "jac":
+            return [f"k_safe_action_jac<{solver}, {mode}, {K}, true, {bs}>", f"k_apply_jac<{1 if mode == 0 else 2}, {bs}>"]
         return [f"k_safe_action<{solver}, {mode}, {K}, true, {bs}>", f"k_safe_action_bwd<{solver}, {mode}, {K}, true, {bs}>"]
     return [f"k_safe_step<{solver}, {mode}, {K}, false, {bs}, false>"]
 
@@ -560,8 +567,10 @@ def main():
     launch = ("no kernel (CPU dry run)" if args.cpu_dry_run else "eager launches" if args.no_graph
               else f"{S} launches from one host call" if args.launch == "seq" else f"hipGraph of {S} steps")
     sac = args.workload == "sac_update"
-    what = ("RCBF_SAC.get_safe_action forward + backward on a replay batch (rcbf_obs_safe_action + "
-            "rcbf_obs_safe_action_backward, diff CBF-QP, implicit-KKT grad)" if sac else
+    what = (("RCBF_SAC.get_safe_action forward + backward on a replay batch (" +
+             ("rcbf_obs_safe_action_jac + rcbf_safe_action_apply_jac" if args.sac_bwd == "jac" else
+              "rcbf_obs_safe_action + rcbf_obs_safe_action_backward") +
+             ", diff CBF-QP, implicit-KKT grad)") if sac else
             "fused safe step (rcbf_safe_step), non-diff CBF-QP")
     rec = {
         "metric": METRICS.get(args.config, METRICS[0]),
@@ -741,18 +750,25 @@ def setup_sac_update(args, dev, rank, B):
     ws = [torch.randn(B, env.n_u, device=dev, generator=gen).contiguous() for _ in range(npool)]
     uo = torch.empty(B, env.n_u, device=dev)
     gu = torch.empty(B, env.n_u, device=dev)
+    jac = torch.empty(B, env.n_u, env.n_u, dtype=torch.float64, device=dev)
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     prm = ctypes.byref(layer._prm)
+    p = _lib.ptr
 
     def steps(n, off=0):
         s = _lib.stream_of(dev)
         for j in range(n):
             k = (off + j) % npool
-            _lib.check(lib.rcbf_obs_safe_action(prm, B, _lib.ptr(obs), _lib.ptr(us[k]), None, None, _lib.ptr(uo),
-                                                None, _lib.ptr(flag), s), "rcbf_obs_safe_action")
-            _lib.check(lib.rcbf_obs_safe_action_backward(prm, B, _lib.ptr(obs), _lib.ptr(us[k]), None, None,
-                                                         _lib.ptr(ws[k]), _lib.ptr(gu), s),
-                       "rcbf_obs_safe_action_backward")
+            if args.sac_bwd == "jac":
+                _lib.check(lib.rcbf_obs_safe_action_jac(prm, B, p(obs), p(us[k]), None, None, p(uo), p(jac), None,
+                                                        p(flag), s), "rcbf_obs_safe_action_jac")
+                _lib.check(lib.rcbf_safe_action_apply_jac(B, env.n_u, p(jac), p(ws[k]), p(gu), s),
+                           "rcbf_safe_action_apply_jac")
+            else:
+                _lib.check(lib.rcbf_obs_safe_action(prm, B, p(obs), p(us[k]), None, None, p(uo), None, p(flag), s),
+                           "rcbf_obs_safe_action")
+                _lib.check(lib.rcbf_obs_safe_action_backward(prm, B, p(obs), p(us[k]), None, None, p(ws[k]), p(gu),
+                                                             s), "rcbf_obs_safe_action_backward")
     steps(1)
     torch.cuda.synchronize()
     active_frac = float((uo != us[0]).any(1).float().mean().item())

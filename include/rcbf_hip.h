@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 9
+#define RCBF_ABI_VERSION 10
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -179,6 +179,25 @@ int rcbf_obs_safe_action(const rcbf_params* prm, int64_t B, const float* obs,
 int rcbf_obs_safe_action_backward(const rcbf_params* prm, int64_t B, const float* obs,
                                   const float* u_rl, const float* mu, const float* sigma,
                                   const float* grad_u, float* grad_u_rl, hipStream_t stream);
+
+/* rcbf_safe_action / rcbf_obs_safe_action that also keep what their
+ * backward needs, as qpth's QPFunction keeps its solution for the backward
+ * (the forward the SAC update differentiates, sac_cbf.py:147-158): u_out
+ * exactly as the plain forward, plus jac_out (B, n_u, n_u) f64 =
+ * d final / d u_rl on the exact active set, through the normaliser, with the
+ * clamp folded in (a saturated action's row is NaN, "no gradient").
+ * rcbf_safe_action_apply_jac is then the whole backward: grad_u_rl =
+ * grad_u . jac over the non-NaN rows, bit for bit what
+ * rcbf_[obs_]safe_action_backward computes, without the second solve. */
+int rcbf_safe_action_jac(const rcbf_params* prm, int64_t B, const float* x, const float* u_rl,
+                         const float* mu, const float* sigma, float* u_out, double* jac_out,
+                         int32_t* status_out, int32_t* fail_flag, hipStream_t stream);
+int rcbf_obs_safe_action_jac(const rcbf_params* prm, int64_t B, const float* obs,
+                             const float* u_rl, const float* mu, const float* sigma, float* u_out,
+                             double* jac_out, int32_t* status_out, int32_t* fail_flag,
+                             hipStream_t stream);
+int rcbf_safe_action_apply_jac(int64_t B, int32_t n_u, const double* jac, const float* grad_u,
+                               float* grad_u_rl, hipStream_t stream);
 
 /* CascadeCBFLayer.get_u_safe (cbf_qp.py:29-53), fp64 batched: build ->
  * normalise -> exact QP.  Returns u_qp only (caller adds u_nom, no clamp). */

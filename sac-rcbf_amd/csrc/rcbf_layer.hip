@@ -137,18 +137,15 @@ __global__ void __launch_bounds__(BS) k_safe_action(rcbf_params prm, int64_t B, 
 // backward passes where lo <= v <= hi).  dh_r/du_c is closed form:
 //   CBF rows: dh/du = Lg (cars) or a_j (unicycle) = -G_raw[r][c];
 //   actuator rows (u_max - u, -u_min + u): -1 / +1.
-template <int SOLVER, int MODE, int K, bool FROM_OBS = false, int BS = kBlock>
-__global__ void __launch_bounds__(BS) k_safe_action_bwd(rcbf_params prm, int64_t B, const float* __restrict__ x,
-                                                            const float* __restrict__ u, const float* __restrict__ mu,
-                                                            const float* __restrict__ sigma,
-                                                            const float* __restrict__ grad_u,
-                                                            float* __restrict__ grad_u_rl) {
+// J[a][c] = d(u_a + z_a) / d u_c; pass[a]: the clamp passes action a's gradient.
+template <int SOLVER, int MODE, int K>
+__device__ __forceinline__ void layer_jacobian(const rcbf_params& prm, const float* xs, const float* us,
+                                               const float* m, const float* s,
+                                               double (&J)[Dims<MODE, K>::NU][Dims<MODE, K>::NU],
+                                               bool (&pass)[Dims<MODE, K>::NU]) {
     using D = Dims<MODE, K>;
     constexpr int N = D::N, M = D::M, NU = D::NU;
-    int64_t i = env_index<BS>();
-    if (i >= B) return;
-    float xs[D::NS], us[NU], m[D::NS], s[D::NS], uf[NU];
-    load_layer_inputs<MODE, K, FROM_OBS>(i, x, u, mu, sigma, xs, us, m, s);
+    float uf[NU];
     LayerState<MODE, K> L;
     layer_forward<SOLVER, MODE, K, true>(prm, xs, us, m, s, uf, L);
     double pd[N];
@@ -175,7 +172,6 @@ __global__ void __launch_bounds__(BS) k_safe_action_bwd(rcbf_params prm, int64_t
         }
         nact += a ? 1 : 0;
     }
-    double J[NU][NU];  // J[a][c] = d(u_a + z_a)/d u_c
 #pragma unroll
     for (int c = 0; c < NU; ++c) {
         double dGn[M][N], dhn[M];
@@ -260,13 +256,81 @@ __global__ void __launch_bounds__(BS) k_safe_action_bwd(rcbf_params prm, int64_t
         for (int a = 0; a < NU; ++a) J[a][c] = (a == c ? 1.0 : 0.0) + dz[a];
     }
 #pragma unroll
+    for (int a = 0; a < NU; ++a) {
+        float v = us[a] + (float)L.qp.z[a];
+        pass[a] = (v >= (float)prm.u_min[a]) && (v <= (float)prm.u_max[a]);
+    }
+}
+
+// the backward, recomputing the forward: grad_u_rl_c = sum over the passing a of grad_u_a J[a][c]
+template <int SOLVER, int MODE, int K, bool FROM_OBS = false, int BS = kBlock>
+__global__ void __launch_bounds__(BS) k_safe_action_bwd(rcbf_params prm, int64_t B, const float* __restrict__ x,
+                                                        const float* __restrict__ u, const float* __restrict__ mu,
+                                                        const float* __restrict__ sigma,
+                                                        const float* __restrict__ grad_u,
+                                                        float* __restrict__ grad_u_rl) {
+    using D = Dims<MODE, K>;
+    constexpr int NU = D::NU;
+    int64_t i = env_index<BS>();
+    if (i >= B) return;
+    float xs[D::NS], us[NU], m[D::NS], s[D::NS];
+    load_layer_inputs<MODE, K, FROM_OBS>(i, x, u, mu, sigma, xs, us, m, s);
+    double J[NU][NU];
+    bool pass[NU];
+    layer_jacobian<SOLVER, MODE, K>(prm, xs, us, m, s, J, pass);
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        double acc = 0.0;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) acc += pass[a] ? (double)grad_u[i * NU + a] * J[a][c] : 0.0;
+        grad_u_rl[i * NU + c] = (float)acc;
+    }
+}
+
+// The forward that also keeps what its backward needs (like qpth's
+// QPFunction keeping zhats): u_out exactly as k_safe_action, plus the
+// Jacobian (B, n_u, n_u) f64 with the clamp folded in (a saturated action's
+// row holds NaN: "no gradient"), so the backward is one small elementwise
+// launch (k_apply_jac) instead of a second solve; it computes what
+// k_safe_action_bwd computes, bit for bit.
+template <int SOLVER, int MODE, int K, bool FROM_OBS = false, int BS = kBlock>
+__global__ void __launch_bounds__(BS) k_safe_action_jac(rcbf_params prm, int64_t B, const float* __restrict__ x,
+                                                        const float* __restrict__ u, const float* __restrict__ mu,
+                                                        const float* __restrict__ sigma, float* __restrict__ u_out,
+                                                        double* __restrict__ jac, int32_t* __restrict__ status_out,
+                                                        int32_t* fail_flag) {
+    using D = Dims<MODE, K>;
+    constexpr int NU = D::NU;
+    int64_t i = env_index<BS>();
+    if (i >= B) return;
+    float xs[D::NS], us[NU], m[D::NS], s[D::NS], uf[NU];
+    load_layer_inputs<MODE, K, FROM_OBS>(i, x, u, mu, sigma, xs, us, m, s);
+    LayerState<MODE, K> L;
+    layer_forward<SOLVER, MODE, K>(prm, xs, us, m, s, uf, L);
+#pragma unroll
+    for (int c = 0; c < NU; ++c) u_out[i * NU + c] = uf[c];
+    report(L.qp.status, status_out, i, fail_flag);
+    double J[NU][NU];
+    bool pass[NU];
+    layer_jacobian<SOLVER, MODE, K>(prm, xs, us, m, s, J, pass);
+#pragma unroll
+    for (int a = 0; a < NU; ++a)
+#pragma unroll
+        for (int c = 0; c < NU; ++c) jac[(i * NU + a) * NU + c] = pass[a] ? J[a][c] : __builtin_nan("");
+}
+
+template <int NU, int BS>
+__global__ void __launch_bounds__(BS) k_apply_jac(int64_t B, const double* __restrict__ jac,
+                                                  const float* __restrict__ grad_u, float* __restrict__ grad_u_rl) {
+    int64_t i = env_index<BS>();
+    if (i >= B) return;
+#pragma unroll
     for (int c = 0; c < NU; ++c) {
         double acc = 0.0;
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
-            float v = us[a] + (float)L.qp.z[a];
-            bool pass = (v >= (float)prm.u_min[a]) && (v <= (float)prm.u_max[a]);
-            acc += pass ? (double)grad_u[i * NU + a] * J[a][c] : 0.0;
+            const double j = jac[(i * NU + a) * NU + c];
+            acc += isnan(j) ? 0.0 : (double)grad_u[i * NU + a] * j;
         }
         grad_u_rl[i * NU + c] = (float)acc;
     }
@@ -343,6 +407,42 @@ int rcbf_obs_safe_action_backward(const rcbf_params* prm, int64_t B, const float
     if (!obs || !u_rl || !grad_u || !grad_u_rl) return RCBF_E_NULL;
     RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action_bwd<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs,
                                       u_rl, mu, sigma, grad_u, grad_u_rl));
+    return launch_status();
+}
+
+int rcbf_safe_action_jac(const rcbf_params* prm, int64_t B, const float* x, const float* u_rl, const float* mu,
+                         const float* sigma, float* u_out, double* jac_out, int32_t* status_out, int32_t* fail_flag,
+                         hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !u_rl || !u_out || !jac_out) return RCBF_E_NULL;
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action_jac<SOLVER_, MODE_, K_, false, BS_>), stream, *prm, B, x, u_rl,
+                                      mu, sigma, u_out, jac_out, status_out, fail_flag));
+    return launch_status();
+}
+
+int rcbf_obs_safe_action_jac(const rcbf_params* prm, int64_t B, const float* obs, const float* u_rl,
+                             const float* mu, const float* sigma, float* u_out, double* jac_out,
+                             int32_t* status_out, int32_t* fail_flag, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!obs || !u_rl || !u_out || !jac_out) return RCBF_E_NULL;
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action_jac<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs,
+                                      u_rl, mu, sigma, u_out, jac_out, status_out, fail_flag));
+    return launch_status();
+}
+
+int rcbf_safe_action_apply_jac(int64_t B, int32_t n_u, const double* jac, const float* grad_u, float* grad_u_rl,
+                               hipStream_t stream) {
+    if (B < 0 || (n_u != 1 && n_u != 2)) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!jac || !grad_u || !grad_u_rl) return RCBF_E_NULL;
+    if (n_u == 1)
+        RCBF_BS_LAUNCH(B, (k_apply_jac<1, BS_>), stream, B, jac, grad_u, grad_u_rl);
+    else
+        RCBF_BS_LAUNCH(B, (k_apply_jac<2, BS_>), stream, B, jac, grad_u, grad_u_rl);
     return launch_status();
 }
 

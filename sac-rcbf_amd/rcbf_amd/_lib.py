@@ -23,7 +23,7 @@ SOLVER_PDIPM = 1
 SOLVER_GI = 2
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NONFINITE = 0, 1, 2, 3
 MAX_HAZARDS = 8
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL"}
 
@@ -87,6 +87,9 @@ SIGNATURES = {
     "rcbf_gp_predict": [_GPM, _I64, _P, _P, _P, _P, _P],
     "rcbf_gp_predict_cols": [_GPM, _I64, _P, _P, _P, _P, _I32, _P, _P, _P, _P],
     "rcbf_obs_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_safe_action_jac": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_obs_safe_action_jac": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_safe_action_apply_jac": [_I64, _I32, _P, _P, _P, _P],
     "rcbf_cascade_u_safe": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_env_reset": [_PRM, _I64, _P, _P, _U64, _I64, _P, _P, _P, _P, _P, _P],
     "rcbf_env_step": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
@@ -161,7 +164,8 @@ def _bind_fast(lib):
 
 
 TORCH_OP_ENTRY_POINTS = ("rcbf_safe_action", "rcbf_safe_action_backward", "rcbf_obs_safe_action",
-                         "rcbf_obs_safe_action_backward")
+                         "rcbf_obs_safe_action_backward", "rcbf_safe_action_jac", "rcbf_obs_safe_action_jac",
+                         "rcbf_safe_action_apply_jac")
 _torch_op = None
 
 

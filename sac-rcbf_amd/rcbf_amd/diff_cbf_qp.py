@@ -58,7 +58,9 @@ def _raise_if_failed(flag):
 
 class _SafeAction(torch.autograd.Function):
     """final = clamp(u + QP(u)[:n_u]);  grad flows to `u` only, like the
-    reference whose state/mean/sigma arrive detached (dynamics.py:211,362)."""
+    reference whose state/mean/sigma arrive detached (dynamics.py:211,362).
+    When u needs a gradient the forward keeps d final / d u per row
+    (rcbf_[obs_]safe_action_jac) and the backward is rcbf_safe_action_apply_jac."""
 
     @staticmethod
     def forward(ctx, layer, x, u, mu, sigma, from_obs=False):
@@ -66,22 +68,41 @@ class _SafeAction(torch.autograd.Function):
         B = x.shape[0]
         out = torch.empty_like(u)
         flag = _fail_flag(layer, x.device) if layer.check_failures else None
-        fn = lib.rcbf_obs_safe_action if from_obs else lib.rcbf_safe_action
-        rc = fn(ctypes.byref(layer._prm), B, _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu), _lib.ptr(sigma),
-                _lib.ptr(out), None, _lib.ptr(flag), _lib.stream_of(x.device))
-        _lib.check(rc, "rcbf_obs_safe_action" if from_obs else "rcbf_safe_action")
+        want_jac = bool(ctx.needs_input_grad[2])
+        if want_jac:
+            jac = torch.empty(B, u.shape[1], u.shape[1], dtype=torch.float64, device=u.device)
+            fn = lib.rcbf_obs_safe_action_jac if from_obs else lib.rcbf_safe_action_jac
+            rc = fn(ctypes.byref(layer._prm), B, _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu), _lib.ptr(sigma),
+                    _lib.ptr(out), _lib.ptr(jac), None, _lib.ptr(flag), _lib.stream_of(x.device))
+            _lib.check(rc, "rcbf_obs_safe_action_jac" if from_obs else "rcbf_safe_action_jac")
+        else:
+            fn = lib.rcbf_obs_safe_action if from_obs else lib.rcbf_safe_action
+            rc = fn(ctypes.byref(layer._prm), B, _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu), _lib.ptr(sigma),
+                    _lib.ptr(out), None, _lib.ptr(flag), _lib.stream_of(x.device))
+            _lib.check(rc, "rcbf_obs_safe_action" if from_obs else "rcbf_safe_action")
         if layer.check_failures:
             _raise_if_failed(flag)
         ctx.layer = layer
         ctx.from_obs = from_obs
-        ctx.save_for_backward(x, u, mu, sigma)
+        ctx.want_jac = want_jac
+        if want_jac:
+            ctx.save_for_backward(jac)
+        else:
+            ctx.save_for_backward(x, u, mu, sigma)
         return out
 
     @staticmethod
     def backward(ctx, grad):
-        x, u, mu, sigma = ctx.saved_tensors
         lib = _lib.load()
         g = grad.contiguous().to(torch.float32)
+        if ctx.want_jac:
+            (jac,) = ctx.saved_tensors
+            gu = torch.empty_like(g)
+            rc = lib.rcbf_safe_action_apply_jac(jac.shape[0], jac.shape[1], _lib.ptr(jac), _lib.ptr(g), _lib.ptr(gu),
+                                                _lib.stream_of(jac.device))
+            _lib.check(rc, "rcbf_safe_action_apply_jac")
+            return None, None, gu, None, None, None
+        x, u, mu, sigma = ctx.saved_tensors
         gu = torch.empty_like(u)
         fn = lib.rcbf_obs_safe_action_backward if ctx.from_obs else lib.rcbf_safe_action_backward
         rc = fn(ctypes.byref(ctx.layer._prm), x.shape[0], _lib.ptr(x), _lib.ptr(u), _lib.ptr(mu), _lib.ptr(sigma),

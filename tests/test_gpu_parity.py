@@ -129,6 +129,52 @@ def test_sac_update_safe_action_from_obs(mode, B):
     assert torch.equal(out.detach(), out2.detach()) and torch.equal(uu.grad, u2.grad)
 
 
+@pytest.mark.parametrize("mode,k", [("SimulatedCars", 0), ("Unicycle", 3), ("Unicycle", 5)])
+@pytest.mark.parametrize("from_obs", [False, True])
+def test_jacobian_forward_equals_resolving_backward(mode, k, from_obs):
+    """rcbf_[obs_]safe_action_jac (the forward the autograd op runs when the
+    action needs a gradient) writes the plain forward's u bit for bit, and
+    rcbf_safe_action_apply_jac on its Jacobian gives the re-solving backward
+    (rcbf_[obs_]safe_action_backward) bit for bit, clamped actions included;
+    B = 4096 + 37 (small-batch workgroups, ragged tail), per-env mean/sigma."""
+    import ctypes
+    from rcbf_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(17 + k + 100 * from_obs)
+    B = 4096 + 37
+    hz = O.UNI["hazards"][:k] if mode == "Unicycle" else None
+    env = _env(mode, hz)
+    layer = _layer(env, 20.0)
+    if mode == "SimulatedCars":
+        x, _, _ = _cars_states(B, 5)
+        obs = O.cars_obs(x).astype(np.float32)
+    else:
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        obs = O.uni_obs(x).astype(np.float32)
+    s32 = O.get_state_f32(mode, obs)
+    inp = dev(obs if from_obs else s32)
+    n_u = env.n_u
+    u = dev(rng.uniform(-3, 3, (B, n_u)))  # beyond the box: some actions saturate the clamp
+    mu = dev(0.01 * rng.normal(0, 1, (B, env.n_s)))
+    sg = dev(0.2 * rng.uniform(0, 1, (B, env.n_s)) + 0.05)
+    g = dev(rng.normal(0, 1, (B, n_u)))
+    out_a, out_b = torch.empty_like(u), torch.empty_like(u)
+    jac = torch.empty(B, n_u, n_u, dtype=torch.float64, device="cuda")
+    ga, gb = torch.empty_like(u), torch.empty_like(u)
+    prm, s = ctypes.byref(layer._prm), _lib.stream_of(u.device)
+    p = _lib.ptr
+    pre = "rcbf_obs_safe_action" if from_obs else "rcbf_safe_action"
+    assert getattr(lib, pre)(prm, B, p(inp), p(u), p(mu), p(sg), p(out_a), None, None, s) == 0
+    assert getattr(lib, pre + "_jac")(prm, B, p(inp), p(u), p(mu), p(sg), p(out_b), p(jac), None, None, s) == 0
+    assert getattr(lib, pre + "_backward")(prm, B, p(inp), p(u), p(mu), p(sg), p(g), p(ga), s) == 0
+    assert lib.rcbf_safe_action_apply_jac(B, n_u, p(jac), p(g), p(gb), s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out_a, out_b)
+    assert torch.equal(ga, gb)
+    saturated = torch.isnan(jac).any(2).any(1)
+    assert 0 < int(saturated.sum()) < B  # both kinds of rows occur
+
+
 def test_solve_qp_and_cbf_layer_surface(golden):
     d = golden("cars_layer")
     layer = _layer(_env("SimulatedCars"), float(d["gamma_b"]))
