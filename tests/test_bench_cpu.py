@@ -1,0 +1,76 @@
+"""bench.py's measurement plumbing on the CPU (no kernel): the config
+presets, the kernel names it looks up in rocprofv3 summaries, the committed
+profiles it reads `frac_rocprof` / `traffic` from, and the dry-run JSON line
+of every config."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _args(*argv):
+    old = sys.argv
+    sys.argv = ["bench.py", *argv]
+    try:
+        return bench.parse()
+    finally:
+        sys.argv = old
+
+
+@pytest.mark.parametrize("cfg,env,batch,workload,scaling", [
+    (0, "SimulatedCars", 65536, "step", "weak"), (1, "SimulatedCars", 1, "step", "weak"),
+    (2, "SimulatedCars", 4096, "step", "weak"), (3, "Unicycle", 4096, "step", "weak"),
+    (4, "SimulatedCars", 262144, "step", "strong"), (5, "SimulatedCars", 4096, "sac_update", "weak")])
+def test_config_presets_follow_baseline_json(cfg, env, batch, workload, scaling):
+    a = _args("--config", str(cfg))
+    assert (a.env, a.batch, a.workload, a.scaling) == (env, batch, workload, scaling)
+    if cfg == 3:
+        assert a.hazards == 3  # BASELINE config 3: the 3-obstacle constraint set
+
+
+def test_block_size_mirrors_the_library():
+    # rcbf_common.hpp block_for_envs: 256 from 65 536 envs, 128 from 32 768, else 64
+    assert [bench.block_for_envs(b) for b in (1, 4096, 32767, 32768, 65535, 65536, 262144)] == \
+        [64, 64, 64, 128, 128, 256, 256]
+
+
+def test_kernel_names_and_profile_lookup():
+    a = _args()
+    assert bench.workload_short(a) == "cars"
+    assert bench.dominant_kernels(a, 65536) == ["k_safe_step<0, 0, 1, false, 256, false>"]
+    a3 = _args("--config", "3")
+    assert bench.workload_short(a3) == "uni3"
+    assert bench.dominant_kernels(a3, 4096) == ["k_safe_step<0, 1, 3, false, 64, false>"]
+    a5 = _args("--config", "5")
+    assert bench.workload_short(a5) == "sacupd_cars"
+    assert bench.dominant_kernels(a5, 4096) == ["k_safe_action_jac<0, 0, 1, true, 64>", "k_apply_jac<1, 64>"]
+    # the committed r04 summaries of the headline are found and parsed
+    us, src = bench.rocprof_kernel_us("cars", 65536, bench.dominant_kernels(a, 65536))
+    assert src and src.startswith("profiles/r") and 2.0 < us < 20.0
+    tr, tsrc = bench.pmc_traffic_file("cars", 65536)
+    assert tsrc and 0.9 < tr / (241 * 65536) < 1.5
+    # a kernel name no summary holds gives None, never another kernel's time
+    assert bench.rocprof_kernel_us("cars", 65536, ["k_not_a_kernel<0>"]) == (None, None)
+
+
+@pytest.mark.parametrize("cfg", [0, 2, 5])
+def test_dry_run_line_carries_the_contract_fields(cfg):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-dry-run", "--steps", "5",
+                        "--warmup", "1", "--config", str(cfg)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in rec, k
+    rf = rec["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_us_rocprof", "frac_rocprof",
+              "rocprof_source"):
+        assert k in rf, k
+    assert rec["config"]["baseline_config"] == (cfg or None)
+    assert rf["bytes_per_env_step"] == (56 if cfg == 5 else 241)
