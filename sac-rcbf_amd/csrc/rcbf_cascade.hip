@@ -1,0 +1,66 @@
+// rcbf_cascade.hip -- the Cascade layer (CascadeCBFLayer.get_u_safe,
+// cbf_qp.py:29-53) + C-ABI: rcbf_cascade_u_safe.
+#include "rcbf_common.hpp"
+
+using namespace rcbf;
+
+namespace {
+
+template <int SOLVER, int MODE, int K>
+__global__ void __launch_bounds__(kBlock) k_cascade(rcbf_params prm, int64_t B, const double* __restrict__ un,
+                                                    const double* __restrict__ x, const double* __restrict__ mu,
+                                                    const double* __restrict__ sigma, double* __restrict__ u_out,
+                                                    int32_t* __restrict__ status_out, int32_t* fail_flag) {
+    using D = Dims<MODE, K>;
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= B) return;
+    double xs[D::NS], us[D::NU], m[D::NS], s[D::NS];
+#pragma unroll
+    for (int k = 0; k < D::NS; ++k) {
+        xs[k] = x[i * D::NS + k];
+        m[k] = mu ? mu[i * D::NS + k] : 0.0;
+        s[k] = sigma ? sigma[i * D::NS + k] : (double)prior_sigma<MODE>(k);
+    }
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) us[c] = un[i * D::NU + c];
+    double G[D::M][D::N], h[D::M], Nrm[D::M];
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS)
+        cars_rows_cascade(prm, xs, us[0], G, h);
+    else
+        uni_rows_cascade<K>(prm, xs, us, m, s, G, h);
+    normalize_rows<D::N, D::M, double>(G, h, Nrm, nullptr);  // cbf_qp.py:270-273
+    double pd[D::N], q[D::N];
+    cascade_P<MODE>(pd);
+#pragma unroll
+    for (int k = 0; k < D::N; ++k) q[k] = 0.0;
+    PMat<D::N, true> pm;
+    pmat_set_diag<D::N>(pm, pd);
+    QPResult<D::N, D::M> res;
+    if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && SOLVER == RCBF_SOLVER_ACTIVE_SET)
+        cars_qp_1d<double>(pm, G, h, res.z, res.status);
+    else if constexpr (MODE == RCBF_MODE_UNICYCLE && SOLVER == RCBF_SOLVER_ACTIVE_SET)
+        uni_qp_2d<K, double>(pm, G, h, res.z, res.status);
+    else
+        qp_solve<SOLVER, D::N, D::M, true, double>(pm, q, G, h, prm.max_iter, prm.eps, res);
+#pragma unroll
+    for (int c = 0; c < D::NU; ++c) u_out[i * D::NU + c] = res.z[c];
+    report(res.status, status_out, i, fail_flag);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom, const double* x, const double* mu,
+                        const double* sigma, double* u_safe_out, int32_t* status_out, int32_t* fail_flag,
+                        hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!x || !u_nom || !u_safe_out) return RCBF_E_NULL;
+    RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_cascade<SOLVER_, MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0, stream,
+                                          *prm, B, u_nom, x, mu, sigma, u_safe_out, status_out, fail_flag));
+    return launch_status();
+}
+
+}  // extern "C"
