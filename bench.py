@@ -43,9 +43,10 @@ PRIOR_TENSOR_BYTES = {"SimulatedCars": 12, "Unicycle": 24}
 
 
 def bytes_per_step(args):
+    prior = PRIOR_TENSOR_BYTES[args.env] if args.prior in ("tensor", "rows") else 0
     if args.workload == "sac_update":
-        return SAC_UPDATE_BYTES[args.env]
-    return BYTES_PER_STEP[args.env] + (PRIOR_TENSOR_BYTES[args.env] if args.prior in ("tensor", "rows") else 0)
+        return SAC_UPDATE_BYTES[args.env] + prior
+    return BYTES_PER_STEP[args.env] + prior
 
 
 def parse():
@@ -87,20 +88,25 @@ def parse():
                     help="step: the fused safe step; sac_update: RCBF_SAC.get_safe_action on a replay batch "
                          "forward + backward (rcbf_obs_safe_action + its backward, config 5)")
     ap.add_argument("--no-span", action="store_true", help="skip the untimed in-kernel span measurement")
+    ap.add_argument("--prior-values", default="posterior", choices=["posterior", "maxstd"],
+                    help="values of the per-env mean/sigma tensors (--prior rows/tensor): posterior = a fitted GP's "
+                         "stand-in (small mean, sigma near MAX_STD); maxstd = mean 0, sigma = MAX_STD materialised per "
+                         "env, as predict_disturbance returns them before any fit (SURVEY 8(d) configs 2 and 5)")
     ap.add_argument("--sac-bwd", default="jac", choices=["jac", "resolve"],
                     help="config 5's backward: jac = the forward keeps d final / d u (rcbf_obs_safe_action_jac) and "
                          "the backward applies it (rcbf_safe_action_apply_jac), as the autograd op runs it; resolve "
                          "= the plain forward and the re-solving backward (rcbf_obs_safe_action_backward)")
     args = ap.parse_args()
     preset = {1: dict(env="SimulatedCars", batch=1, workload="step"),
-              2: dict(env="SimulatedCars", batch=4096, workload="step"),
+              2: dict(env="SimulatedCars", batch=4096, workload="step", prior="rows", prior_values="maxstd"),
               3: dict(env="Unicycle", hazards=3, batch=4096, workload="step"),
               4: dict(env="SimulatedCars", batch=262144, scaling="strong", workload="step"),
-              5: dict(env="SimulatedCars", batch=4096, workload="sac_update")}.get(args.config, {})
+              5: dict(env="SimulatedCars", batch=4096, workload="sac_update", prior="rows",
+                      prior_values="maxstd")}.get(args.config, {})
     for k, v in preset.items():
         setattr(args, k, v)
-    if args.workload == "sac_update" and (args.prior != "prior" or args.launch != "graph" or args.no_graph):
-        raise SystemExit("--workload sac_update runs the prior, hipGraph-launched")
+    if args.workload == "sac_update" and (args.prior == "tensor" or args.launch != "graph" or args.no_graph):
+        raise SystemExit("--workload sac_update reads (B, n_s) rows or the in-kernel prior, hipGraph-launched")
     return args
 
 
@@ -362,10 +368,10 @@ def block_for_envs(B):
 
 def workload_short(args):
     """The workload's name in profiles/ file names."""
-    base = "cars" if args.env == "SimulatedCars" else f"uni{args.hazards}"
-    if args.workload == "sac_update":
-        return "sacupd_" + base
-    return base + {"prior": "", "tensor": "_tensorprior", "rows": "_rowsprior"}[args.prior]
+    base = ("sacupd_" if args.workload == "sac_update" else "") + ("cars" if args.env == "SimulatedCars"
+                                                                  else f"uni{args.hazards}")
+    return base + {"prior": "", "tensor": "_tensorprior", "rows": "_rowsprior"}[args.prior] + \
+        ("_maxstd" if args.prior != "prior" and args.prior_values == "maxstd" else "")
 
 
 def dominant_kernels(args, B):
@@ -567,6 +573,12 @@ def main():
     launch = ("no kernel (CPU dry run)" if args.cpu_dry_run else "eager launches" if args.no_graph
               else f"{S} launches from one host call" if args.launch == "seq" else f"hipGraph of {S} steps")
     sac = args.workload == "sac_update"
+    prior_text = {"prior": "prior mean/sigma in-kernel",
+                  "tensor": "per-env mean/sigma, column layout of rcbf_gp_predict_cols",
+                  "rows": "per-env mean/sigma (B, n_s) row tensors"}[args.prior] + (
+        "" if args.prior == "prior" else
+        " (mean 0, sigma = MAX_STD materialised, before the GP fit)" if args.prior_values == "maxstd" else
+        " (post-GP-fit stand-in)")
     what = (("RCBF_SAC.get_safe_action forward + backward on a replay batch (" +
              ("rcbf_obs_safe_action_jac + rcbf_safe_action_apply_jac" if args.sac_bwd == "jac" else
               "rcbf_obs_safe_action + rcbf_obs_safe_action_backward") +
@@ -587,12 +599,8 @@ def main():
         "dtype": "f32 rows / f64 QP" if sac else "f32 rows / f64 QP / f64 env",
         "data": ("dry run: launcher and collectives only, no kernel, not a measurement" if args.cpu_dry_run else
                  "synthetic (fp32 observations of SURVEY 8(d) states one env step on, policy actions ~ U[-1,1], "
-                 "upstream gradient ~ N(0,1), prior mean/sigma)" if sac else
-                 "synthetic (SURVEY 8(d) start states, u_RL ~ U[-1,1], "
-                 + {"prior": "prior mean/sigma",
-                    "tensor": "per-env mean/sigma, column layout of rcbf_gp_predict_cols (post-GP-fit regime)",
-                    "rows": "per-env mean/sigma (B, n_s) row tensors (post-GP-fit regime)"}[args.prior]
-                 + ", seeded auto-resets)"),
+                 "upstream gradient ~ N(0,1), " + prior_text + ")" if sac else
+                 "synthetic (SURVEY 8(d) start states, u_RL ~ U[-1,1], " + prior_text + ", seeded auto-resets)"),
         "config": {"workload": f"{args.env} {what}, {hz}"
                                f"batch {B} envs per GPU, {args.solver} fp64 QP, {launch}",
                    "baseline_config": args.config or None,
@@ -639,6 +647,19 @@ def unicycle_hazards(k):
     return _EnvSpec("Unicycle").hazards_locations[:k]
 
 
+def prior_tensors(args, env, gen):
+    """Per-env (B, n_s) mean / sigma rows for --prior rows / tensor."""
+    B, dev = env.num_envs, env.device
+    if args.prior_values == "maxstd":  # predict_disturbance before any fit (dynamics.py:381-384), materialised
+        from rcbf_amd.dynamics import MAX_STD
+        sigma = torch.tensor(MAX_STD[args.env], dtype=torch.float32, device=dev).repeat(B, 1).contiguous()
+        return torch.zeros(B, env.n_s, device=dev), sigma
+    # a fitted GP's per-env posterior (dynamics.py:342-390): small mean, sigma near MAX_STD
+    mean = (0.01 * torch.randn(B, env.n_s, device=dev, generator=gen)).contiguous()
+    sigma = (0.2 * torch.rand(B, env.n_s, device=dev, generator=gen) + 0.05).contiguous()
+    return mean, sigma
+
+
 def setup_gpu(args, dev, rank, B):
     """Untimed set-up of the measured workload on this rank's GPU: envs at
     SURVEY start states, the layer, a pool of u_RL batches, warm-up, and the
@@ -666,8 +687,7 @@ def setup_gpu(args, dev, rank, B):
     mean = sigma = None
     layout = "cols" if args.prior == "tensor" else "rows"
     if args.prior in ("tensor", "rows"):  # a fitted GP's per-env posterior (dynamics.py:342-390): small mean, sigma near MAX_STD
-        mean = (0.01 * torch.randn(B, env.n_s, device=dev, generator=gen)).contiguous()
-        sigma = (0.2 * torch.rand(B, env.n_s, device=dev, generator=gen) + 0.05).contiguous()
+        mean, sigma = prior_tensors(args, env, gen)
         if layout == "cols":  # what GPDisturbanceModel.predict_cols writes for the step
             cols = list(env.PRIOR_COLS[args.env])
             sigma = sigma[:, cols].t().contiguous()
@@ -748,6 +768,9 @@ def setup_sac_update(args, dev, rank, B):
     npool = min(S, 50)
     us = [(torch.rand(B, env.n_u, device=dev, generator=gen) * 2 - 1).contiguous() for _ in range(npool)]
     ws = [torch.randn(B, env.n_u, device=dev, generator=gen).contiguous() for _ in range(npool)]
+    mu = sg = None
+    if args.prior == "rows":  # predict_disturbance's (B, n_s) outputs (sac_cbf.py:231-236)
+        mu, sg = prior_tensors(args, env, gen)
     uo = torch.empty(B, env.n_u, device=dev)
     gu = torch.empty(B, env.n_u, device=dev)
     jac = torch.empty(B, env.n_u, env.n_u, dtype=torch.float64, device=dev)
@@ -760,14 +783,14 @@ def setup_sac_update(args, dev, rank, B):
         for j in range(n):
             k = (off + j) % npool
             if args.sac_bwd == "jac":
-                _lib.check(lib.rcbf_obs_safe_action_jac(prm, B, p(obs), p(us[k]), None, None, p(uo), p(jac), None,
+                _lib.check(lib.rcbf_obs_safe_action_jac(prm, B, p(obs), p(us[k]), p(mu), p(sg), p(uo), p(jac), None,
                                                         p(flag), s), "rcbf_obs_safe_action_jac")
                 _lib.check(lib.rcbf_safe_action_apply_jac(B, env.n_u, p(jac), p(ws[k]), p(gu), s),
                            "rcbf_safe_action_apply_jac")
             else:
-                _lib.check(lib.rcbf_obs_safe_action(prm, B, p(obs), p(us[k]), None, None, p(uo), None, p(flag), s),
+                _lib.check(lib.rcbf_obs_safe_action(prm, B, p(obs), p(us[k]), p(mu), p(sg), p(uo), None, p(flag), s),
                            "rcbf_obs_safe_action")
-                _lib.check(lib.rcbf_obs_safe_action_backward(prm, B, p(obs), p(us[k]), None, None, p(ws[k]), p(gu),
+                _lib.check(lib.rcbf_obs_safe_action_backward(prm, B, p(obs), p(us[k]), p(mu), p(sg), p(ws[k]), p(gu),
                                                              s), "rcbf_obs_safe_action_backward")
     steps(1)
     torch.cuda.synchronize()

@@ -47,14 +47,14 @@ wl_kernel() {  # the timed kernel's name in rocprofv3 output (workgroup size fro
     c1|c2) echo 'k_safe_step<0, 0, 1, false, 64, false>' ;;
     c3) echo 'k_safe_step<0, 1, 3, false, 64, false>' ;;
     c4s) echo 'k_safe_step<0, 0, 1, false, 128, false>' ;;
-    c5) echo 'k_safe_action<0, 0, 1, true, 64>' ;;
+    c5) echo 'k_safe_action_jac<0, 0, 1, true, 64>' ;;
   esac
 }
 wl_name() {  # <short>_B<batch>, the workload's name in profiles/ (bench.py workload_short)
   case $1 in cars) echo cars_B65536 ;; uni3) echo uni3_B65536 ;; uni5) echo uni5_B65536 ;;
     carsT) echo cars_tensorprior_B65536 ;; carsR) echo cars_rowsprior_B65536 ;; uni5T) echo uni5_tensorprior_B65536 ;;
-    c1) echo cars_B1 ;; c2) echo cars_B4096 ;; c3) echo uni3_B4096 ;; c4) echo cars_B262144 ;; c4s) echo cars_B32768 ;;
-    c5) echo sacupd_cars_B4096 ;; esac
+    c1) echo cars_B1 ;; c2) echo cars_rowsprior_maxstd_B4096 ;; c3) echo uni3_B4096 ;; c4) echo cars_B262144 ;;
+    c4s) echo cars_B32768 ;; c5) echo sacupd_cars_rowsprior_maxstd_B4096 ;; esac
 }
 for step in "$@"; do
   wl=${step#*_}

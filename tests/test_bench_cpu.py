@@ -48,7 +48,7 @@ def test_kernel_names_and_profile_lookup():
     assert bench.workload_short(a3) == "uni3"
     assert bench.dominant_kernels(a3, 4096) == ["k_safe_step<0, 1, 3, false, 64, false>"]
     a5 = _args("--config", "5")
-    assert bench.workload_short(a5) == "sacupd_cars"
+    assert bench.workload_short(a5) == "sacupd_cars_rowsprior_maxstd"  # MAX_STD materialised per env
     assert bench.dominant_kernels(a5, 4096) == ["k_safe_action_jac<0, 0, 1, true, 64>", "k_apply_jac<1, 64>"]
     # the committed r04 summaries of the headline are found and parsed
     us, src = bench.rocprof_kernel_us("cars", 65536, bench.dominant_kernels(a, 65536))
@@ -73,4 +73,5 @@ def test_dry_run_line_carries_the_contract_fields(cfg):
               "rocprof_source"):
         assert k in rf, k
     assert rec["config"]["baseline_config"] == (cfg or None)
-    assert rf["bytes_per_env_step"] == (56 if cfg == 5 else 241)
+    # configs 2 and 5 read the materialised sigma[5, 7, 9] rows (+12 B)
+    assert rf["bytes_per_env_step"] == {0: 241, 2: 253, 5: 68}[cfg]
