@@ -160,15 +160,17 @@ def cpu_baseline(env_name, hazards, seconds, B=65536):
 
 
 def cpu_sac_update(env_name, hazards, seconds, B):
-    """Config 5's CPU baseline: the numpy oracle's CBFQPLayer forward and its
-    gradient w.r.t. the action (oracle.safe_action_diff / _grad: the
-    reference's fp32 rows, normaliser, exact QP, clamp, implicit-KKT
-    backward) on B rows of observations, numpy on this host (`cores` is the
-    BLAS thread count numpy may use; the loops themselves are vectorised
-    numpy on one core)."""
+    """Config 5's CPU baseline: the C oracle's CBFQPLayer forward and its
+    gradient w.r.t. the action (oracle/rcbf_oracle.c oracle_safe_action_grad,
+    the restatement of oracle.safe_action_diff_grad: fp32 rows, normaliser,
+    exact QP, clamp, implicit-KKT derivative on the active set, OpenMP over
+    rows) on B observations' states of the SURVEY 8(d) distribution, prior
+    mean/sigma; 1 thread, then the median of 3 samples on all threads."""
+    from oracle import c_oracle as C
     from oracle import oracle as O
     rng = np.random.default_rng(3)
     hz = O.UNI["hazards"][:hazards] if env_name == "Unicycle" else None
+    threads_all = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     if env_name == "SimulatedCars":  # SURVEY 8(d) states: seeded resets advanced 0-299 steps under u ~ U[-1, 1]
         x, t, st = O.cars_reset(rng.normal(0, 0.5, B))
         stop = rng.integers(0, 300, B)
@@ -185,19 +187,30 @@ def cpu_sac_update(env_name, hazards, seconds, B):
     s32 = O.get_state_f32(env_name, obs)
     mu, sg = O.predict_disturbance_prior(env_name, B)
     mu, sg = mu.astype(np.float32), sg.astype(np.float32)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        u = rng.uniform(-1, 1, (B, n_u)).astype(np.float32)
-        w = rng.normal(0, 1, (B, n_u)).astype(np.float32)
-        O.safe_action_diff(env_name, s32, u, mu, sg, 20.0, hazards=hz)
-        O.safe_action_diff_grad(env_name, s32, u, mu, sg, 20.0, w, hazards=hz)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": round(n * B / el, 1), "unit": "safe actions/s (forward + backward)", "cores": 1, "kind": "port",
-            "sample": f"numpy oracle CBFQPLayer forward + d/du backward (oracle/oracle.py safe_action_diff, "
-                      f"safe_action_diff_grad), {n} batches x {B} rows in {el:.1f} s"}
+    u = rng.uniform(-1, 1, (B, n_u)).astype(np.float32)
+    w = rng.normal(0, 1, (B, n_u)).astype(np.float32)
+
+    def run(threads, budget):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            C.safe_action_grad(env_name, s32, u, mu, sg, 20.0, w, hazards=hz, threads=threads)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return n * B / el, n, el
+
+    v1, n1, _ = run(1, seconds * 0.25)
+    run(threads_all, min(1.0, seconds * 0.05))  # untimed: the OpenMP pool's start-up
+    samples = [run(threads_all, seconds * 0.25) for _ in range(3)]
+    rates = sorted(v for v, _, _ in samples)
+    nN, eN = sum(n for _, n, _ in samples), sum(e for _, _, e in samples)
+    return {"value": round(rates[1], 1), "unit": "safe actions/s (forward + backward)", "cores": threads_all,
+            "kind": "port",
+            "sample": f"C oracle CBFQPLayer forward + d/du backward (oracle/rcbf_oracle.c oracle_safe_action_grad, "
+                      f"exact QP, implicit-KKT gradient), median of 3 samples on {threads_all} threads "
+                      f"({rates[0]:.4g} / {rates[1]:.4g} / {rates[2]:.4g} actions/s; {nN} batches x {B} rows in "
+                      f"{eN:.1f} s); 1 thread: {v1:.4g} actions/s ({n1} batches)",
+            "spread": [round(r, 1) for r in rates]}
 
 
 def cpu_baselines_in_child(args):

@@ -27,6 +27,8 @@ def lib():
                                           P, P, P, P, P, P, P, P, ctypes.c_int]
         _lib.oracle_safe_step_ex.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double, ctypes.c_int64,
                                              P, P, P, P, P, P, P, P, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int]
+        _lib.oracle_safe_action_grad.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double, ctypes.c_int64,
+                                                 P, P, P, P, P, P, P, ctypes.c_int]
         _lib.oracle_max_threads.restype = ctypes.c_int
     return _lib
 
@@ -51,6 +53,21 @@ def safe_action(mode, x, u, mu, sigma, gamma_b, hazards=None, threads=0):
     fails = lib().oracle_safe_action(m, K, _p(hz), float(gamma_b), x.shape[0], _p(x), _p(u), _p(mu), _p(sigma),
                                      _p(out), int(threads))
     return out, fails
+
+
+def safe_action_grad(mode, x, u, mu, sigma, gamma_b, w, hazards=None, threads=0):
+    """CBFQPLayer.get_safe_action and d(sum w * final)/d u (oracle.safe_action_diff_grad
+    restated in C): returns (final (B, n_u) f32, grad (B, n_u) f64, fails)."""
+    m = 0 if mode == "SimulatedCars" else 1
+    x = np.ascontiguousarray(x, np.float32); u = np.ascontiguousarray(u, np.float32)
+    mu = np.ascontiguousarray(mu, np.float32); sigma = np.ascontiguousarray(sigma, np.float32)
+    w = np.ascontiguousarray(w, np.float32)
+    hz, K = _hz(hazards)
+    out = np.empty_like(u)
+    grad = np.empty(u.shape, np.float64)
+    fails = lib().oracle_safe_action_grad(m, K, _p(hz), float(gamma_b), x.shape[0], _p(x), _p(u), _p(mu), _p(sigma),
+                                          _p(w), _p(out), _p(grad), int(threads))
+    return out, grad, fails
 
 
 def safe_step(mode, x, aux, step, u, gamma_b, hazards=None, threads=0):

@@ -121,8 +121,15 @@ static int solve_k(int k, double A[MAXN][MAXN], double* b, double* x) {
     return 1;
 }
 
-/* min 1/2 z' diag(P) z s.t. G z <= h; returns 0 on success */
+/* min 1/2 z' diag(P) z s.t. G z <= h; returns 0 on success.  [nullable]
+ * S_out / k_out / lam_out: the active rows (row order) and their multipliers. */
+static int qp_exact_as(int m, int n, const double* Pd, float Gf[][MAXN], const float* hf, double* z, int* S_out,
+                       int* k_out, double* lam_out);
 static int qp_exact(int m, int n, const double* Pd, float Gf[][MAXN], const float* hf, double* z) {
+    return qp_exact_as(m, n, Pd, Gf, hf, z, NULL, NULL, NULL);
+}
+static int qp_exact_as(int m, int n, const double* Pd, float Gf[][MAXN], const float* hf, double* z, int* S_out,
+                       int* k_out, double* lam_out) {
     double G[MAXM][MAXN], h[MAXM], scale = 1.0, ah = 0.0, ag = 0.0;
     for (int r = 0; r < m; ++r) {
         h[r] = hf[r];
@@ -207,6 +214,11 @@ static int qp_exact(int m, int n, const double* Pd, float Gf[][MAXN], const floa
                 for (int a = 0; a < k; ++a) if (lam[a] < -tol) dual = 0;
                 if (viol <= tol && dual) {
                     for (int j = 0; j < n; ++j) z[j] = zz[j];
+                    if (k_out) *k_out = k;
+                    for (int a = 0; a < k; ++a) {
+                        if (S_out) S_out[a] = S[a];
+                        if (lam_out) lam_out[a] = lam[a];
+                    }
                     return 0;
                 }
             }
@@ -309,6 +321,127 @@ int oracle_safe_action(int mode, int K, const double* hz, double gamma_b, int64_
                 float v = u[2 * i + c] + (float)z[c];
                 out[2 * i + c] = fminf(fmaxf(v, -2.5f), 2.5f);
             }
+        }
+    }
+    return fails;
+}
+
+/* d(sum w * final)/d u_RL of CBFQPLayer.get_safe_action (oracle.py
+ * safe_action_diff_grad restated): the implicit-function derivative of the
+ * exact QP on its active set A, through the row normaliser (torch.max routes
+ * dN to the first maximal entry of [G_r h_r]) and the clamp mask, fp64:
+ *   P dz + dGn' lam + Gn_A' dlam = 0,  Gn_A dz = dhn_A - dGn_A z,
+ *   grad_c = sum_a mask_a w_a (delta_ac + dz_a^c). */
+static int solve_dense(int k, double A[2 * MAXN][2 * MAXN], double* b, double* x) {
+    for (int c = 0; c < k; ++c) {
+        int p = c;
+        for (int r = c + 1; r < k; ++r) if (fabs(A[r][c]) > fabs(A[p][c])) p = r;
+        if (p != c) {
+            for (int j = 0; j < k; ++j) { double t = A[c][j]; A[c][j] = A[p][j]; A[p][j] = t; }
+            double t = b[c]; b[c] = b[p]; b[p] = t;
+        }
+        if (A[c][c] == 0.0) return 0;
+        for (int r = c + 1; r < k; ++r) {
+            double f = A[r][c] / A[c][c];
+            for (int j = c; j < k; ++j) A[r][j] -= f * A[c][j];
+            b[r] -= f * b[c];
+        }
+    }
+    for (int i = k - 1; i >= 0; --i) {
+        double v = b[i];
+        for (int j = i + 1; j < k; ++j) v -= A[i][j] * x[j];
+        x[i] = v / A[i][i];
+    }
+    return 1;
+}
+
+int oracle_safe_action_grad(int mode, int K, const double* hz, double gamma_b, int64_t B, const float* x,
+                            const float* u, const float* mu, const float* sig, const float* w, float* out,
+                            double* grad, int nthreads) {
+    int fails = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel for schedule(static) reduction(+ : fails)
+    for (int64_t i = 0; i < B; ++i) {
+        const int nu = mode == 0 ? 1 : 2, n = nu + 1, m = mode == 0 ? 4 : K + 4;
+        const float lo = mode == 0 ? -10.0f : -2.5f, hi = -lo;
+        float G[MAXM][MAXN], h[MAXM], Gn[MAXM][MAXN], hn[MAXM];
+        double Pd[MAXN];
+        if (mode == 0) {
+            cars_rows(x + i * 10, u[i], sig + i * 10, gamma_b, G, h);
+            Pd[0] = (double)0.1f; Pd[1] = (double)10.0f;
+        } else {
+            uni_rows(x + i * 3, u + i * 2, mu + i * 3, sig + i * 3, gamma_b, K, hz, G, h);
+            Pd[0] = (double)1.0f; Pd[1] = (double)1e-2f; Pd[2] = (double)1e5f;
+        }
+        memcpy(Gn, G, sizeof(G));
+        memcpy(hn, h, sizeof(h));
+        normalize(m, n, Gn, hn);
+        double z[MAXN], lam[MAXN];
+        int S[MAXN], k = 0;
+        if (qp_exact_as(m, n, Pd, Gn, hn, z, S, &k, lam) != 0) {
+            ++fails;
+            for (int c = 0; c < nu; ++c) { out[i * nu + c] = NAN; grad[i * nu + c] = NAN; }
+            continue;
+        }
+        double lamr[MAXM] = {0};
+        for (int a = 0; a < k; ++a) lamr[S[a]] = lam[a];
+        /* the normaliser's N and which entry torch.max picked (first maximum; |h| wins only if larger) */
+        double Nr[MAXM];
+        int selh[MAXM];
+        for (int r = 0; r < m; ++r) {
+            float mx = fabsf(G[r][0]);
+            int arg = 0;
+            for (int c = 1; c < n; ++c) if (fabsf(G[r][c]) > mx) { mx = fabsf(G[r][c]); arg = c; }
+            if (fabsf(h[r]) > mx) { mx = fabsf(h[r]); arg = n; }
+            Nr[r] = mx;
+            selh[r] = arg == n;
+        }
+        double J[2][2] = {{0}};
+        for (int c = 0; c < nu; ++c) {
+            double dhn[MAXM], dGn[MAXM][MAXN];
+            for (int r = 0; r < m; ++r) {
+                double dh;
+                const int k0 = m - 2 * nu;
+                if (r < k0) dh = -(double)G[r][c];
+                else dh = ((r - k0) / 2 == c) ? (((r - k0) % 2 == 0) ? -1.0 : 1.0) : 0.0;
+                const double sgn = h[r] > 0.0f ? 1.0 : (h[r] < 0.0f ? -1.0 : 0.0);
+                const double dN = selh[r] ? sgn * dh : 0.0;
+                dhn[r] = (dh - (double)hn[r] * dN) / Nr[r];
+                for (int j = 0; j < n; ++j) dGn[r][j] = -(double)Gn[r][j] * (dN / Nr[r]);
+            }
+            double A[2 * MAXN][2 * MAXN] = {{0}}, rhs[2 * MAXN], sol[2 * MAXN];
+            for (int j = 0; j < n; ++j) {
+                A[j][j] = Pd[j];
+                double acc = 0.0;
+                for (int r = 0; r < m; ++r) acc += dGn[r][j] * lamr[r];
+                rhs[j] = -acc;
+            }
+            for (int a = 0; a < k; ++a) {
+                for (int j = 0; j < n; ++j) {
+                    A[j][n + a] = (double)Gn[S[a]][j];
+                    A[n + a][j] = (double)Gn[S[a]][j];
+                }
+                double acc = dhn[S[a]];
+                for (int j = 0; j < n; ++j) acc -= dGn[S[a]][j] * z[j];
+                rhs[n + a] = acc;
+            }
+            if (!solve_dense(n + k, A, rhs, sol)) { ++fails; for (int j = 0; j < n; ++j) sol[j] = NAN; }
+            for (int a = 0; a < nu; ++a) J[a][c] = (a == c ? 1.0 : 0.0) + sol[a];
+        }
+        for (int a = 0; a < nu; ++a) {
+            const float v = u[i * nu + a] + (float)z[a];
+            out[i * nu + a] = fminf(fmaxf(v, lo), hi);
+        }
+        for (int c = 0; c < nu; ++c) {
+            double acc = 0.0;
+            for (int a = 0; a < nu; ++a) {
+                const float v = u[i * nu + a] + (float)z[a];
+                const double mask = (v >= lo && v <= hi) ? 1.0 : 0.0;
+                acc += mask * (double)w[i * nu + a] * J[a][c];
+            }
+            grad[i * nu + c] = acc;
         }
     }
     return fails;

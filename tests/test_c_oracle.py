@@ -88,3 +88,22 @@ def test_c_oracle_fused_step_with_mean_sigma_matches_numpy(mode):
         ref = C.safe_step_ex(mode, xc, ac, sc, u, 20.0, hazards=hz, mean=mu, sigma=sg, threads=2)
         assert ref["fails"] == 0 and rel(ref["u"], fin) <= 1e-5
         assert rel(xc, x) <= 1e-9 and np.array_equal(ref["cost"], np.asarray(c, np.float32))
+
+
+@pytest.mark.parametrize("name,mode", [("cars_layer", "SimulatedCars"), ("unicycle3_layer", "Unicycle"),
+                                       ("unicycle5_layer", "Unicycle")])
+@pytest.mark.parametrize("tag", ["prior", "rand"])
+def test_c_oracle_gradient_matches_reference_fixtures(golden, name, mode, tag):
+    """oracle_safe_action_grad (config 5's CPU baseline) vs the reference's
+    own d final / d u_RL (fixtures made by autograd through the reference's
+    normaliser and clamp) and the numpy oracle's restatement."""
+    d = golden(name)
+    hz = d["hazards"] if mode == "Unicycle" else None
+    x, u, mu, sg, w = (d[tag + k] for k in ("_x", "_u", "_mu", "_sigma", "_w"))
+    out, grad, fails = C.safe_action_grad(mode, x, u, mu, sg, float(d["gamma_b"]), w, hazards=hz, threads=2)
+    assert fails == 0
+    assert rel(out, d[tag + "_final"]) <= 1e-5
+    assert rel(grad, d[tag + "_grad_u"]) <= 1e-5
+    g_np, _ = O.safe_action_diff_grad(mode, x[:300], u[:300], mu[:300], sg[:300], float(d["gamma_b"]), w[:300],
+                                      hazards=hz)
+    assert rel(grad[:300], g_np) <= 1e-9
