@@ -175,6 +175,46 @@ def test_jacobian_forward_equals_resolving_backward(mode, k, from_obs):
     assert 0 < int(saturated.sum()) < B  # both kinds of rows occur
 
 
+@pytest.mark.parametrize("mode,k", [("SimulatedCars", 0), ("Unicycle", 3)])
+def test_config5_workload_vs_c_oracle(mode, k):
+    """Config 5 as bench.py runs it (SURVEY states, MAX_STD
+    materialised per env as (B, n_s) rows, upstream gradient w ~ N(0, 1)):
+    the autograd op's forward (rcbf_obs_safe_action_jac) and backward
+    (rcbf_safe_action_apply_jac) against the C oracle's forward and implicit-
+    KKT gradient (oracle_safe_action_grad), B = 4096."""
+    from oracle import c_oracle as C
+    from rcbf_amd.dynamics import MAX_STD
+    from rcbf_amd.sac_cbf import get_safe_action
+    from rcbf_amd.dynamics import DynamicsModel
+    B = 4096
+    rng = np.random.default_rng(55 + k)
+    hz = O.UNI["hazards"][:k] if mode == "Unicycle" else None
+    env = _env(mode, hz)
+    layer = _layer(env, 20.0)
+    if mode == "SimulatedCars":
+        x, _, _ = _cars_states(B, 9)
+        obs = O.cars_obs(x).astype(np.float32)
+    else:
+        x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+        obs = O.uni_obs(x).astype(np.float32)
+    u = rng.uniform(-1, 1, (B, env.n_u)).astype(np.float32)
+    w = rng.normal(0, 1, (B, env.n_u)).astype(np.float32)
+    mu = np.zeros((B, env.n_s), np.float32)
+    sg = np.tile(np.asarray(MAX_STD[mode], np.float32), (B, 1))
+    uu = dev(u).requires_grad_(True)
+    out = layer.get_safe_action(dev(O.get_state_f32(mode, obs)), uu, dev(mu), dev(sg))
+    (out * dev(w)).sum().backward()
+    ref, g, fails = C.safe_action_grad(mode, O.get_state_f32(mode, obs), u, mu, sg, 20.0, w, hazards=hz, threads=4)
+    assert fails == 0
+    assert rel(out.detach().cpu().numpy(), ref) <= 1e-5
+    assert rel(uu.grad.cpu().numpy(), g) <= 1e-5
+    # the obs-input path of RCBF_SAC.get_safe_action gives the same numbers
+    u2 = dev(u).requires_grad_(True)
+    out2 = get_safe_action(layer, dev(obs), u2, DynamicsModel(env, Args()))
+    (out2 * dev(w)).sum().backward()
+    assert torch.equal(out2.detach(), out.detach()) and torch.equal(u2.grad, uu.grad)
+
+
 def test_solve_qp_and_cbf_layer_surface(golden):
     d = golden("cars_layer")
     layer = _layer(_env("SimulatedCars"), float(d["gamma_b"]))
