@@ -357,7 +357,8 @@ def pin_host_cores(local, n):
 
 METRICS = {
     0: "safe env steps/sec (dynamics+CBF-QP) at batch 65536, 1/2/4/8 MI355X",
-    1: "safe env steps/sec (dynamics+CBF-QP), config 1: SimulatedCars, 1 env",
+    1: "safe env steps/sec (dynamics+CBF-QP), config 1: SimulatedCars, 1 env (the fused CBFQPLayer step; config 1's "
+       "Cascade closed loop is tests/test_gpu_parity.py::test_closed_loop_config1)",
     2: "safe env steps/sec (dynamics+CBF-QP), config 2: SimulatedCars batch 4096, 1 MI355X",
     3: "safe env steps/sec (dynamics+CBF-QP), config 3: Unicycle (3 hazards) batch 4096, 1 MI355X",
     4: "safe env steps/sec (dynamics+CBF-QP), config 4: SimulatedCars batch 262144 over the GPUs",
