@@ -392,7 +392,7 @@ def dominant_kernels(args, B):
     """The kernel(s) one timed step launches, as rocprofv3 names them."""
     solver = 1 if args.solver == "pdipm" else 0
     mode, K = (0, 1) if args.env == "SimulatedCars" else (1, args.hazards)
-    bs = block_for_envs(B)
+    bs = block_for_envs(B) if solver == 0 else 256  # the small workgroups are the exact solver's only
     if args.workload == "sac_update":
         if args.sac_bwd == "jac":
             return [f"k_safe_action_jac<{solver}, {mode}, {K}, true, {bs}>", f"k_apply_jac<{1 if mode == 0 else 2}, {bs}>"]

@@ -457,6 +457,25 @@ inline int launch_status() { return (int)hipGetLastError(); }
         }                                                                                                   \
     } while (0)
 
+// The same for a kernel instantiated per solver: only the exact (default)
+// solver gets the small workgroups; the others always run 256-thread ones (in
+// the small branches BS_ folds to 256 for them, so no extra instantiation).
+#define RCBF_BS_LAUNCH_S(SOLVER, B, KERNEL, stream, ...)                                                      \
+    do {                                                                                                    \
+        constexpr bool exact_ = (SOLVER) == RCBF_SOLVER_ACTIVE_SET;                                         \
+        const int bs_ = exact_ ? rcbf::block_for_envs(B) : 256;                                             \
+        if (bs_ == 256) {                                                                                   \
+            constexpr int BS_ = 256;                                                                        \
+            hipLaunchKernelGGL(KERNEL, dim3(rcbf::grid_for_envs(B, BS_)), dim3(BS_), 0, stream, __VA_ARGS__); \
+        } else if (bs_ == 128) {                                                                            \
+            constexpr int BS_ = exact_ ? 128 : 256;                                                         \
+            hipLaunchKernelGGL(KERNEL, dim3(rcbf::grid_for_envs(B, BS_)), dim3(BS_), 0, stream, __VA_ARGS__); \
+        } else {                                                                                            \
+            constexpr int BS_ = exact_ ? 64 : 256;                                                          \
+            hipLaunchKernelGGL(KERNEL, dim3(rcbf::grid_for_envs(B, BS_)), dim3(BS_), 0, stream, __VA_ARGS__); \
+        }                                                                                                   \
+    } while (0)
+
 // Dispatch a launch over (mode, unicycle hazard count) -> MODE_, K_.
 #define RCBF_DISPATCH_MODE(prm, ...)                                 \
     do {                                                             \

@@ -297,17 +297,22 @@ void launch_k_safe_step(int64_t B, double* x, double* aux, int32_t* step, const 
                         float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out, int32_t* fail_flag,
                         int32_t auto_reset, uint64_t seed, int64_t env_offset, const rcbf_params& prm, int cols,
                         unsigned long long* span, hipStream_t stream) {
-    const int bs = block_for_envs(B);
+    // the exact (default) solver gets the small workgroups; the others run 256-thread ones
+    const int bs = SOLVER == RCBF_SOLVER_ACTIVE_SET ? block_for_envs(B) : 256;
 #define RCBF_SS_L(BS_)                                                                                             \
     hipLaunchKernelGGL((k_safe_step<SOLVER, MODE, K, false, BS_, SPAN>), dim3(grid_for_envs(B, BS_)), dim3(BS_), 0, \
                        stream, B, x, aux, step, u_rl, episode, mu, sigma, obs_out, u_out, reward, cost, done,       \
                        goal_met, status_out, fail_flag, auto_reset, seed, env_offset, prm, cols, span)
-    if (bs == 256)
+    if constexpr (SOLVER != RCBF_SOLVER_ACTIVE_SET) {
         RCBF_SS_L(256);
-    else if (bs == 128)
-        RCBF_SS_L(128);
-    else
-        RCBF_SS_L(64);
+    } else {
+        if (bs == 256)
+            RCBF_SS_L(256);
+        else if (bs == 128)
+            RCBF_SS_L(128);
+        else
+            RCBF_SS_L(64);
+    }
 #undef RCBF_SS_L
 }
 

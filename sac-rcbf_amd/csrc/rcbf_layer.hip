@@ -130,6 +130,109 @@ __global__ void __launch_bounds__(BS) k_safe_action(rcbf_params prm, int64_t B, 
     report(L.qp.status, status_out, i, fail_flag);
 }
 
+// Multipliers of the layer's QP at its closed-form optimum (diagonal P,
+// q = 0, the normalised rows in L): the rows with G_r z = h_r (to 1e-9
+// relative) form A, and lam_A solves P z + G_A' lam_A = 0 on them.  Returns
+// false for a degenerate point (more than n rows tight, a negative multiplier
+// or a stationarity residual); the caller then runs Goldfarb-Idnani.
+template <int MODE, int K>
+__device__ __forceinline__ bool layer_multipliers(const double* pd, LayerState<MODE, K>& L) {
+    using D = Dims<MODE, K>;
+    constexpr int N = D::N, M = D::M;
+    double GA[N][N], ip[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) ip[k] = 1.0 / pd[k];
+    int nact = 0, aidx[N];
+    uint32_t amask = 0;
+    bool ok = true;
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) {
+        aidx[sl] = -1;
+#pragma unroll
+        for (int k = 0; k < N; ++k) GA[sl][k] = 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        double v = -(double)L.h[r];
+#pragma unroll
+        for (int k = 0; k < N; ++k) v = fma((double)L.G[r][k], L.qp.z[k], v);
+        const bool tight = fabs(v) <= 1e-9 * (1.0 + fabs((double)L.h[r]));
+        ok = ok && !(tight && nact >= N);
+        const bool a = tight && nact < N;
+#pragma unroll
+        for (int sl = 0; sl < N; ++sl) {
+            const bool here = a && (sl == nact);
+#pragma unroll
+            for (int k = 0; k < N; ++k) GA[sl][k] = here ? (double)L.G[r][k] : GA[sl][k];
+            aidx[sl] = here ? r : aidx[sl];
+        }
+        amask |= a ? (1u << r) : 0u;
+        nact += a ? 1 : 0;
+    }
+    double S[N][N], w[N], lam[N];
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+#pragma unroll
+        for (int b = 0; b < N; ++b) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc = fma(GA[a][k] * ip[k], GA[b][k], acc);
+            S[a][b] = (a < nact && b < nact) ? acc : (a == b ? 1.0 : 0.0);
+        }
+        w[a] = (a < nact) ? -dotd<N>(GA[a], L.qp.z) : 0.0;
+    }
+    ok = ok && ldl_solve<N>(S, w, lam);
+    double scale = 1.0;
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) scale = fmax(scale, fabs(lam[sl]));
+#pragma unroll
+    for (int sl = 0; sl < N; ++sl) ok = ok && (sl >= nact || lam[sl] >= -1e-9 * scale);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {  // stationarity: P z + G_A' lam = 0
+        double acc = pd[k] * L.qp.z[k];
+#pragma unroll
+        for (int sl = 0; sl < N; ++sl) acc = fma((sl < nact) ? GA[sl][k] : 0.0, lam[sl], acc);
+        ok = ok && fabs(acc) <= 1e-7 * scale * (1.0 + fabs(pd[k] * L.qp.z[k]));
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        double l = 0.0;
+#pragma unroll
+        for (int sl = 0; sl < N; ++sl) l = (sl < nact && aidx[sl] == r) ? fmax(lam[sl], 0.0) : l;
+        L.qp.lam[r] = l;
+    }
+    L.qp.active = amask;
+    L.qp.nact = nact;
+    return ok;
+}
+
+// The forward with multipliers for the backward.  The exact solver (the
+// default): the closed-form optimum on the normalised rows -- the very z the
+// forward returns -- with its multipliers from stationarity; a lane whose
+// point is degenerate re-solves with Goldfarb-Idnani (the rows are the same,
+// so it finds the same optimum).  Other solvers: their own multipliers.
+template <int SOLVER, int MODE, int K>
+__device__ __forceinline__ void layer_forward_lam(const rcbf_params& prm, const float* xs, const float* us,
+                                                  const float* m, const float* s, float* uf,
+                                                  LayerState<MODE, K>& L) {
+    using D = Dims<MODE, K>;
+    if constexpr (SOLVER == RCBF_SOLVER_ACTIVE_SET) {
+        layer_forward<SOLVER, MODE, K>(prm, xs, us, m, s, uf, L);  // normalised rows, closed form
+        double pd[D::N];
+        diff_P<MODE>(pd);
+        if (!layer_multipliers<MODE, K>(pd, L)) {
+            PMat<D::N, true> pm;
+            double q[D::N];
+#pragma unroll
+            for (int k = 0; k < D::N; ++k) q[k] = 0.0;
+            pmat_set_diag<D::N>(pm, pd);
+            qp_solve<SOLVER, D::N, D::M, true, float>(pm, q, L.G, L.h, prm.max_iter, prm.eps, L.qp);
+        }
+    } else {
+        layer_forward<SOLVER, MODE, K, true>(prm, xs, us, m, s, uf, L);
+    }
+}
+
 // d(final)/d(u_rl) on the active set of the exact optimum: the implicit-KKT
 // derivative qpth's QPFunction.backward approximates (D = lam/s over all
 // rows), through the row normaliser (torch.max routes dN to its argmax, the h
@@ -137,17 +240,18 @@ __global__ void __launch_bounds__(BS) k_safe_action(rcbf_params prm, int64_t B, 
 // backward passes where lo <= v <= hi).  dh_r/du_c is closed form:
 //   CBF rows: dh/du = Lg (cars) or a_j (unicycle) = -G_raw[r][c];
 //   actuator rows (u_max - u, -u_min + u): -1 / +1.
-// J[a][c] = d(u_a + z_a) / d u_c; pass[a]: the clamp passes action a's gradient.
+// J[a][c] = d(u_a + z_a) / d u_c; pass[a]: the clamp passes action a's gradient;
+// uf / status: the forward's output (the plain forward's, bit for bit).
 template <int SOLVER, int MODE, int K>
 __device__ __forceinline__ void layer_jacobian(const rcbf_params& prm, const float* xs, const float* us,
                                                const float* m, const float* s,
                                                double (&J)[Dims<MODE, K>::NU][Dims<MODE, K>::NU],
-                                               bool (&pass)[Dims<MODE, K>::NU]) {
+                                               bool (&pass)[Dims<MODE, K>::NU], float* uf, int& status) {
     using D = Dims<MODE, K>;
     constexpr int N = D::N, M = D::M, NU = D::NU;
-    float uf[NU];
     LayerState<MODE, K> L;
-    layer_forward<SOLVER, MODE, K, true>(prm, xs, us, m, s, uf, L);
+    layer_forward_lam<SOLVER, MODE, K>(prm, xs, us, m, s, uf, L);
+    status = L.qp.status;
     double pd[N];
     diff_P<MODE>(pd);
     // active rows (slots) of the solution
@@ -277,7 +381,9 @@ __global__ void __launch_bounds__(BS) k_safe_action_bwd(rcbf_params prm, int64_t
     load_layer_inputs<MODE, K, FROM_OBS>(i, x, u, mu, sigma, xs, us, m, s);
     double J[NU][NU];
     bool pass[NU];
-    layer_jacobian<SOLVER, MODE, K>(prm, xs, us, m, s, J, pass);
+    float uf[NU];
+    int status;
+    layer_jacobian<SOLVER, MODE, K>(prm, xs, us, m, s, J, pass, uf, status);
 #pragma unroll
     for (int c = 0; c < NU; ++c) {
         double acc = 0.0;
@@ -305,14 +411,13 @@ __global__ void __launch_bounds__(BS) k_safe_action_jac(rcbf_params prm, int64_t
     if (i >= B) return;
     float xs[D::NS], us[NU], m[D::NS], s[D::NS], uf[NU];
     load_layer_inputs<MODE, K, FROM_OBS>(i, x, u, mu, sigma, xs, us, m, s);
-    LayerState<MODE, K> L;
-    layer_forward<SOLVER, MODE, K>(prm, xs, us, m, s, uf, L);
-#pragma unroll
-    for (int c = 0; c < NU; ++c) u_out[i * NU + c] = uf[c];
-    report(L.qp.status, status_out, i, fail_flag);
     double J[NU][NU];
     bool pass[NU];
-    layer_jacobian<SOLVER, MODE, K>(prm, xs, us, m, s, J, pass);
+    int status;
+    layer_jacobian<SOLVER, MODE, K>(prm, xs, us, m, s, J, pass, uf, status);
+#pragma unroll
+    for (int c = 0; c < NU; ++c) u_out[i * NU + c] = uf[c];
+    report(status, status_out, i, fail_flag);
 #pragma unroll
     for (int a = 0; a < NU; ++a)
 #pragma unroll
@@ -369,7 +474,7 @@ int rcbf_safe_action(const rcbf_params* prm, int64_t B, const float* x, const fl
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !u_rl || !u_out) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action<SOLVER_, MODE_, K_, false, BS_>), stream, *prm, B, x, u_rl, mu,
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH_S(SOLVER_, B, (k_safe_action<SOLVER_, MODE_, K_, false, BS_>), stream, *prm, B, x, u_rl, mu,
                                       sigma, u_out, status_out, fail_flag));
     return launch_status();
 }
@@ -381,7 +486,7 @@ int rcbf_safe_action_backward(const rcbf_params* prm, int64_t B, const float* x,
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !u_rl || !grad_u || !grad_u_rl) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action_bwd<SOLVER_, MODE_, K_, false, BS_>), stream, *prm, B, x, u_rl,
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH_S(SOLVER_, B, (k_safe_action_bwd<SOLVER_, MODE_, K_, false, BS_>), stream, *prm, B, x, u_rl,
                                       mu, sigma, grad_u, grad_u_rl));
     return launch_status();
 }
@@ -393,7 +498,7 @@ int rcbf_obs_safe_action(const rcbf_params* prm, int64_t B, const float* obs, co
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!obs || !u_rl || !u_out) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs, u_rl, mu,
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH_S(SOLVER_, B, (k_safe_action<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs, u_rl, mu,
                                       sigma, u_out, status_out, fail_flag));
     return launch_status();
 }
@@ -405,7 +510,7 @@ int rcbf_obs_safe_action_backward(const rcbf_params* prm, int64_t B, const float
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!obs || !u_rl || !grad_u || !grad_u_rl) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action_bwd<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs,
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH_S(SOLVER_, B, (k_safe_action_bwd<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs,
                                       u_rl, mu, sigma, grad_u, grad_u_rl));
     return launch_status();
 }
@@ -417,7 +522,7 @@ int rcbf_safe_action_jac(const rcbf_params* prm, int64_t B, const float* x, cons
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !u_rl || !u_out || !jac_out) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action_jac<SOLVER_, MODE_, K_, false, BS_>), stream, *prm, B, x, u_rl,
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH_S(SOLVER_, B, (k_safe_action_jac<SOLVER_, MODE_, K_, false, BS_>), stream, *prm, B, x, u_rl,
                                       mu, sigma, u_out, jac_out, status_out, fail_flag));
     return launch_status();
 }
@@ -429,7 +534,7 @@ int rcbf_obs_safe_action_jac(const rcbf_params* prm, int64_t B, const float* obs
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!obs || !u_rl || !u_out || !jac_out) return RCBF_E_NULL;
-    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH(B, (k_safe_action_jac<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs,
+    RCBF_DISPATCH(prm, RCBF_BS_LAUNCH_S(SOLVER_, B, (k_safe_action_jac<SOLVER_, MODE_, K_, true, BS_>), stream, *prm, B, obs,
                                       u_rl, mu, sigma, u_out, jac_out, status_out, fail_flag));
     return launch_status();
 }

@@ -107,6 +107,7 @@ for step in "$@"; do
         env $lib timeout -k 10 200 python scripts/gp_bench.py 10 3000 > "$OUT/gp_${n}_$r.log" 2>&1 || exit 1
         echo "$n $(tail -1 "$OUT/gp_${n}_$r.log")" >> "$OUT/gpab_sum.txt"
       done; done ;;
+    abjac) bash scripts/ab_multi.sh "$TAG/abjac" "jacgi" c5 || exit 1 ;;
     abbs)  bash scripts/ab_multi.sh "$TAG/abbs" "bs256" c2 c3 c4s c5 || exit 1 ;;
     absin) bash scripts/ab_multi.sh "$TAG/absin" "nosincos" u5 u3 || exit 1 ;;
     *) log "unknown step $step" ;;
