@@ -131,18 +131,18 @@ class _QP(torch.autograd.Function):
     through the normaliser like torch autograd through diff_cbf_qp.py:103-106."""
 
     @staticmethod
-    def forward(ctx, layer, normalize, P, q, G, h):
+    def forward(ctx, layer, prm, normalize, P, q, G, h):
         lib = _lib.load()
         B, m, n = G.shape
         z = torch.empty(B, n, device=G.device)
         z64 = torch.empty(B, n, dtype=torch.float64, device=G.device)  # kept for the backward, like qpth's zhats
         flag = _fail_flag(layer, G.device)
-        rc = lib.rcbf_qp_solve_saved(ctypes.byref(layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G),
+        rc = lib.rcbf_qp_solve_saved(ctypes.byref(prm), B, n, m, _lib.ptr(P), _lib.ptr(q), _lib.ptr(G),
                                      _lib.ptr(h), int(normalize), _lib.ptr(z), _lib.ptr(z64), None, _lib.ptr(flag),
                                      _lib.stream_of(G.device))
         _lib.check(rc, "rcbf_qp_solve_saved")
         _raise_if_failed(flag)
-        ctx.layer = layer
+        ctx.prm = prm
         ctx.normalize = normalize
         ctx.save_for_backward(P, q, G, h, z64)
         return z
@@ -157,12 +157,12 @@ class _QP(torch.autograd.Function):
         gq = torch.empty(B, n, device=G.device) if (need[3] and q is not None) else None
         gG = torch.empty_like(G) if need[4] else None
         gh = torch.empty_like(h) if need[5] else None
-        rc = _lib.load().rcbf_qp_backward_saved(ctypes.byref(ctx.layer._prm), B, n, m, _lib.ptr(P), _lib.ptr(q),
+        rc = _lib.load().rcbf_qp_backward_saved(ctypes.byref(ctx.prm), B, n, m, _lib.ptr(P), _lib.ptr(q),
                                                 _lib.ptr(G), _lib.ptr(h), int(ctx.normalize), _lib.ptr(z64),
                                                 _lib.ptr(gz), _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh),
                                                 _lib.stream_of(G.device))
         _lib.check(rc, "rcbf_qp_backward_saved")
-        return None, None, gP, gq, gG, gh
+        return None, None, None, gP, gq, gG, gh
 
 
 def _divide_rows_in_place(Gs, hs):
@@ -179,6 +179,10 @@ def _divide_rows_in_place(Gs, hs):
         with torch.no_grad():
             Ghs = torch.cat((Gs, hs.to(Gs.dtype).unsqueeze(2)), -1)
             Gs.div_(torch.max(torch.abs(Ghs), dim=2, keepdim=True)[0])
+
+
+# qpth.qp.QPFunction.__init__'s keyword arguments (what cbf_layer's solver_args may carry)
+_QPFUNCTION_ARGS = ("eps", "verbose", "notImprovedLim", "maxIter", "solver", "check_Q_spd")
 
 
 class CBFQPLayer:
@@ -279,11 +283,35 @@ class CBFQPLayer:
 
     # -- diff_cbf_qp.py:111-144 --------------------------------------------
     def cbf_layer(self, Qs, ps, Gs, hs, As=None, bs=None, solver_args=None):
+        """`solver_args` are qpth QPFunction's keyword arguments, as the
+        reference passes them (diff_cbf_qp.py:132-139; solve_qp sends
+        check_Q_spd, maxIter, notImprovedLim, eps, :107).  An unknown key
+        raises TypeError, as QPFunction(**solver_args) does.  With the
+        interior-point solver (solver=SOLVER_PDIPM) `maxIter` and `eps` set its
+        iteration cap and stopping tolerance (notImprovedLim is the
+        reference's 10); the exact solvers return the optimum whatever the
+        tolerance, so they read none of them."""
+        prm = self._solver_params(solver_args)
         if As is not None and As.numel() > 0:
             raise NotImplementedError("equality constraints are not used on this path (diff_cbf_qp.py:135-137)")
-        return self._qp(Qs, ps, Gs, hs, normalize=False)
+        return self._qp(Qs, ps, Gs, hs, normalize=False, prm=prm)
 
-    def _qp(self, Ps, qs, Gs, hs, normalize):
+    def _solver_params(self, solver_args):
+        if not solver_args:
+            return self._prm
+        for k in solver_args:
+            if k not in _QPFUNCTION_ARGS:
+                raise TypeError(f"QPFunction.__init__() got an unexpected keyword argument '{k}'")
+        if self._prm.solver != _lib.SOLVER_PDIPM or ("maxIter" not in solver_args and "eps" not in solver_args):
+            return self._prm
+        prm = _lib.RcbfParams.from_buffer_copy(self._prm)
+        if "maxIter" in solver_args:
+            prm.max_iter = int(solver_args["maxIter"])
+        if "eps" in solver_args:
+            prm.eps = float(solver_args["eps"])
+        return prm
+
+    def _qp(self, Ps, qs, Gs, hs, normalize, prm=None):
         dev = _dev()
         G, h = _f32_keep_grad(Gs, dev), _f32_keep_grad(hs, dev)
         if G.dim() != 3 or h.shape != G.shape[:2]:
@@ -297,7 +325,7 @@ class CBFQPLayer:
             q = q.expand(B, n).contiguous()
         if P.shape != (B, n, n) or (q is not None and q.shape != (B, n)):
             raise ValueError("P must be (B,n,n) and q (B,n)")
-        z = _QP.apply(self, bool(normalize), P, q, G, h)
+        z = _QP.apply(self, self._prm if prm is None else prm, bool(normalize), P, q, G, h)
         od = Gs.device if torch.is_tensor(Gs) else self.device
         return z.to(od)
 

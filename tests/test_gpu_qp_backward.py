@@ -140,6 +140,29 @@ def test_solve_qp_autograd_with_pdipm_layer(normalize):
     assert rel(out.detach().cpu().numpy()[ok], want["z"][ok][:, :out.shape[1]]) <= 1e-5
 
 
+def test_cbf_layer_solver_args_reach_the_interior_point():
+    """cbf_layer(..., solver_args) as the reference passes them to qpth's
+    QPFunction (diff_cbf_qp.py:107,139): with solver=PDIPM, maxIter and eps
+    become the kernel's iteration cap and tolerance.  A capped run (maxIter=2)
+    stops early and its uncertified lanes are re-solved exactly, so every
+    setting returns the optimum."""
+    from rcbf_amd import _lib
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv
+    rng = np.random.default_rng(41)
+    B, n, m = 512, 3, 7
+    P, q, G, h = random_qps(rng, B, n, m)
+    layer = CBFQPLayer(BatchedSimulatedCarsEnv(4), Args(), gamma_b=20.0, solver=_lib.SOLVER_PDIPM)
+    want = O.qp_backward(P, q, G, h, False, np.zeros((B, n), np.float32))["z"]
+    ok = _non_degenerate(P, q, G, h, False)
+    for args in (None, {"check_Q_spd": False, "maxIter": 100000, "notImprovedLim": 10, "eps": 1e-4},
+                 {"maxIter": 2}, {"eps": 1e-12, "verbose": 0}):
+        z = layer.cbf_layer(dev(P), dev(q), dev(G), dev(h), solver_args=args)
+        assert rel(z.cpu().numpy()[ok], want[ok]) <= 1e-5, args
+    with pytest.raises(TypeError):
+        layer.cbf_layer(dev(P), dev(q), dev(G), dev(h), solver_args={"max_iter": 5})
+
+
 @pytest.mark.parametrize("fixture,mode", [("cars_layer", "SimulatedCars"), ("unicycle3_layer", "Unicycle"),
                                           ("unicycle5_layer", "Unicycle")])
 def test_solve_qp_grad_composes_to_reference_grad(golden, fixture, mode):

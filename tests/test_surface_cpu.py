@@ -69,3 +69,29 @@ def test_parameter_names_match_the_reference(key):
     sig = inspect.signature(fn).parameters
     for extra in params[len(ref):]:
         assert sig[extra].default is not inspect.Parameter.empty, (key, extra)
+
+
+def test_cbf_layer_solver_args_follow_qpfunction():
+    """solver_args carry qpth QPFunction's keywords (diff_cbf_qp.py:132-139):
+    an unknown key raises TypeError before any device work; the exact solver
+    reads none of them, the interior point takes maxIter / eps into a copy of
+    its parameters (the layer's own record is untouched)."""
+    from types import SimpleNamespace
+
+    import numpy as np
+
+    from rcbf_amd import _lib
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    box = SimpleNamespace(low=np.full(1, -10.0, np.float32), high=np.full(1, 10.0, np.float32), shape=(1,))
+    env = SimpleNamespace(dynamics_mode="SimulatedCars", safe_action_space=box, action_space=box, kp=4.0,
+                          k_brake=20.0)
+    exact = CBFQPLayer(env, SimpleNamespace(cuda=False), gamma_b=20.0)
+    with pytest.raises(TypeError, match="unexpected keyword argument 'maxiter'"):
+        exact.cbf_layer(None, None, None, None, solver_args={"maxiter": 5})
+    ref_args = {"check_Q_spd": False, "maxIter": 100000, "notImprovedLim": 10, "eps": 1e-4}  # diff_cbf_qp.py:107
+    assert exact._solver_params(ref_args) is exact._prm
+    pd = CBFQPLayer(env, SimpleNamespace(cuda=False), gamma_b=20.0, solver=_lib.SOLVER_PDIPM)
+    p = pd._solver_params(ref_args)
+    assert p is not pd._prm and (p.max_iter, p.eps) == (100000, 1e-4) and (pd._prm.max_iter, pd._prm.eps) == (0, 0.0)
+    assert p.gamma_b == pd._prm.gamma_b and p.solver == _lib.SOLVER_PDIPM
+    assert pd._solver_params({"verbose": 0}) is pd._prm
