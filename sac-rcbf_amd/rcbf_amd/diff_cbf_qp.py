@@ -153,10 +153,11 @@ class _QP(torch.autograd.Function):
         B, m, n = G.shape
         need = ctx.needs_input_grad
         gz = grad_z.to(torch.float32).contiguous()
-        gP = torch.empty_like(P) if need[2] else None
-        gq = torch.empty(B, n, device=G.device) if (need[3] and q is not None) else None
-        gG = torch.empty_like(G) if need[4] else None
-        gh = torch.empty_like(h) if need[5] else None
+        # inputs: layer, prm, normalize, P, q, G, h
+        gP = torch.empty_like(P) if need[3] else None
+        gq = torch.empty(B, n, device=G.device) if (need[4] and q is not None) else None
+        gG = torch.empty_like(G) if need[5] else None
+        gh = torch.empty_like(h) if need[6] else None
         rc = _lib.load().rcbf_qp_backward_saved(ctypes.byref(ctx.prm), B, n, m, _lib.ptr(P), _lib.ptr(q),
                                                 _lib.ptr(G), _lib.ptr(h), int(ctx.normalize), _lib.ptr(z64),
                                                 _lib.ptr(gz), _lib.ptr(gP), _lib.ptr(gq), _lib.ptr(gG), _lib.ptr(gh),
