@@ -27,6 +27,25 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kGpRows = 128;   // query rows per workgroup
 constexpr int kGpCols = 128;   // Rt columns per workgroup
 constexpr int kGpChunk = 256;  // training rows staged in LDS at a time
+#ifndef RCBF_GP_DOT_MFMA
+#define RCBF_GP_DOT_MFMA 0
+#endif
+// Distance dot products on the MFMA (see gp_qform_body): per 32 training
+// rows, 32 x 32 arguments from one augmented product of K = D + 2 (padded
+// to even), instead of D VALU FMAs per k-step.
+constexpr bool kGpDot = RCBF_GP_DOT_MFMA != 0;
+// ... and (level 2) the B operand [R | alpha] staged once per workgroup in
+// LDS by global_load_lds (two 32-row buffers), instead of each wave loading
+// the same rows into its own registers.
+constexpr bool kGpStageRt = RCBF_GP_DOT_MFMA >= 2;
+constexpr int kGpRtBuf = kGpStageRt ? 2 * 32 * kGpCols : 1;  // floats
+template <int D>
+struct GpAug {
+    static constexpr int KA = (D + 2 + 1) / 2 * 2;    // [q0 | 1 | 2 L2E xs] . [1 | tn | xt], padded to even
+    static constexpr int KS = KA / 2;                 // k-steps of the 32x32x2 product
+    static constexpr int KSP = (KS + 3) / 4 * 4;      // per-half LDS stride (16-B reads)
+    static constexpr int F4 = kGpDot ? 2 * KSP / 4 : (D + 3) / 4;  // float4s per staged training row
+};
 
 // Workgroup (row tile of 128 queries, column block cb of 128, GP i): wave w
 // owns query rows 32w..32w+31 and all 128 columns (4 tiles of 32 x 32), so
@@ -51,10 +70,195 @@ constexpr int kGpChunk = 256;  // training rows staged in LDS at a time
 // the epilogue.  One v_fma_f64 per k-step beside four MFMAs.
 // MEAN: this workgroup's column block holds the mean column r (a separate
 // instantiation, so the other ~95 % of the workgroups run the plain loop).
+// This lane's B operand of the dot product: element 2 f + half of
+// [q0, 1, 2 L2E xs, 0...].  The values pass through an empty asm first, so the
+// half-select stays a select of two registers (folded into a select of two
+// array slots it becomes a dynamic index, i.e. a scratch array).
+template <int D>
+__device__ __forceinline__ void gp_query_operand(const float (&xs2)[D], float q0, int half,
+                                                 float (&qb)[GpAug<D>::KS]) {
+    using A = GpAug<D>;
+    float qa[A::KA];
+#pragma unroll
+    for (int e = 0; e < A::KA; ++e) {
+        qa[e] = e == 0 ? q0 : (e == 1 ? 1.0f : (e - 2 < D ? xs2[e - 2] : 0.0f));
+        asm volatile("" : "+v"(qa[e]));
+    }
+#pragma unroll
+    for (int f = 0; f < A::KS; ++f) qb[f] = half ? qa[2 * f + 1] : qa[2 * f];
+}
+
+// The training loop with the distance dot products on the MFMA (kGpDot).
+// Per block of 32 training rows t and the wave's 32 query rows b, one
+// v_mfma_f32_32x32x2_f32 product over the augmented vectors
+//   arg(t, b) = [1, tn_t, xt_t] . [q0_b, 1, 2 L2E xs_b]
+// (K = D + 2, padded to even; KS k-steps) leaves arg(t, b) in the C layout:
+// lane l, register r holds t = (r & 3) + 8 (r >> 2) + 4 (l >> 5), b = l & 31.
+// That is exactly the A-operand layout of the main product's k-step r (query
+// l & 31, training row t for the lane's half), so each k-step costs one
+// fminf + exp2 per lane (the A value) beside its 4 MFMAs, and the B operand
+// of k-step r is Rt row t -- rows 8 g + 4 half + j of the block in group g =
+// r >> 2, j = r & 3.  The augmented order (q0 + tn first, then the D
+// products) is the order of the VALU chain it replaces.
+template <int D, bool SK, bool HAS_MEAN>
+__device__ __forceinline__ void gp_qform_dot_loop(const rcbf_gp_model& m, int i, int n_beg, int n_end,
+                                                  const float (&xs2)[D], float q0, float log2s, const float* Rt_i,
+                                                  const float* alpha_i, const float* xt_i, const float* tn2_i,
+                                                  int64_t ldc, int half, int l32, f32x16* acc, double& macc,
+                                                  float4* s_xt, float* s_alpha) {
+    using A = GpAug<D>;
+    constexpr float kL2E = 1.4426950408889634f;
+    float* s_ta = reinterpret_cast<float*>(s_xt);
+    // this lane's B operand of the dot product: element 2 f + half of [q0, 1, 2 L2E xs, 0...]
+    float qb[A::KS];
+    gp_query_operand<D>(xs2, q0, half, qb);
+    const float* rp = Rt_i + (int64_t)(n_beg + 4 * half) * ldc;  // row 8 gi + j of the range, this half
+    // one 4-deep ring of B values per k-step slot j = r & 3: k-step r's slot
+    // is refilled with k-step r + 4's row right after its MFMAs issue
+    float bv[4][4];
+    auto ldb = [&](int64_t row, float* dst) {
+        const float4 v = *reinterpret_cast<const float4*>(rp + row * ldc);
+        dst[0] = v.x, dst[1] = v.y, dst[2] = v.z, dst[3] = v.w;
+    };
+    for (int n0 = n_beg; n0 < n_end; n0 += kGpChunk) {
+        const int nch = min(kGpChunk, n_end - n0);  // multiple of 32
+        __syncthreads();
+        for (int e = threadIdx.x; e < nch; e += 256) {
+            float ta[A::KA];
+            ta[0] = 1.0f;
+            ta[1] = -kL2E * tn2_i[n0 + e];
+#pragma unroll
+            for (int k = 0; k < A::KA - 2; ++k) ta[2 + k] = k < D ? xt_i[(int64_t)(n0 + e) * D + k] : 0.0f;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int f = 0; f < A::KSP; ++f) s_ta[e * 2 * A::KSP + h * A::KSP + f] = f < A::KS ? ta[2 * f + h] : 0.0f;
+            if constexpr (HAS_MEAN) s_alpha[e] = alpha_i[(int64_t)(n0 + e) * ldc];
+        }
+        __syncthreads();
+        const int64_t base = n0 - n_beg;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ldb(base + j, bv[j]);
+        const int nblk = nch / 32;
+#pragma unroll 1
+        for (int blk = 0; blk < nblk; ++blk) {
+            const float* tp = s_ta + (blk * 32 + l32) * 2 * A::KSP + half * A::KSP;
+            float af[A::KS];
+#pragma unroll
+            for (int f = 0; f < A::KS; ++f) af[f] = tp[f];
+            f32x16 dd;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dd[r] = 0.0f;
+#pragma unroll
+            for (int f = 0; f < A::KS; ++f) dd = __builtin_amdgcn_mfma_f32_32x32x2f32(af[f], qb[f], dd, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                // the group of k-step r + 4 in this chunk; past the chunk's end the ring reloads the
+                // chunk's last group (branch-free; the values are not used)
+                const int gn = min(blk * 4 + g + 1, nblk * 4 - 1);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float av = __builtin_amdgcn_exp2f(fminf(dd[4 * g + j], log2s));
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[j][c], acc[c], 0, 0, 0);
+                    if constexpr (HAS_MEAN) macc = fma((double)av, (double)s_alpha[blk * 32 + 8 * g + 4 * half + j], macc);
+                    ldb(base + 8 * gn + j, bv[j]);
+                }
+            }
+        }
+    }
+}
+
+// Level 2 of gp_qform_dot_loop: block bg's 32 x 128 slice of Rt (16 KB) is
+// copied to LDS buffer bg & 1 by the whole workgroup with 4 global_load_lds
+// (16 B per lane, lane-linear: one wave-instruction = 2 rows) while block
+// bg - 1 is computed; one barrier per block.  The k-step r B value of lane
+// (l32, half) is then a ds_read_b128 of row 8 g + 4 half + j.
+template <int D, bool SK, bool HAS_MEAN>
+__device__ __forceinline__ void gp_qform_dot_staged(const rcbf_gp_model& m, int i, int cb, int n_beg, int n_end,
+                                                    const float (&xs2)[D], float q0, float log2s, const float* alpha_i,
+                                                    const float* xt_i, const float* tn2_i, int64_t ldc, int half,
+                                                    int l32, f32x16* acc, double& macc, float4* s_xt,
+                                                    float* s_alpha, float* s_rt) {
+    using A = GpAug<D>;
+    constexpr float kL2E = 1.4426950408889634f;
+    float* s_ta = reinterpret_cast<float*>(s_xt);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float qb[A::KS];
+    gp_query_operand<D>(xs2, q0, half, qb);
+    const float* Rt_cb = m.Rt + (int64_t)i * m.N_pad * ldc + (int64_t)cb * kGpCols;  // this column block
+    auto issue_rt = [&](int bg) {  // block bg of the range -> buffer bg & 1
+        float* buf = s_rt + (bg & 1) * 32 * kGpCols;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = (q * 4 + w) * 64 + lane;  // float4 index in the 32 x 32 float4 image
+            const float* src = Rt_cb + (int64_t)(n_beg + 32 * bg + (e >> 5)) * ldc + 4 * (e & 31);
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(buf + (q * 4 + w) * 256),
+                                             16, 0, 0);
+        }
+    };
+    auto stage_ta = [&](int n0, int nch) {
+        for (int e = threadIdx.x; e < nch; e += 256) {
+            float ta[A::KA];
+            ta[0] = 1.0f;
+            ta[1] = -kL2E * tn2_i[n0 + e];
+#pragma unroll
+            for (int k = 0; k < A::KA - 2; ++k) ta[2 + k] = k < D ? xt_i[(int64_t)(n0 + e) * D + k] : 0.0f;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int f = 0; f < A::KSP; ++f) s_ta[e * 2 * A::KSP + h * A::KSP + f] = f < A::KS ? ta[2 * f + h] : 0.0f;
+            if constexpr (HAS_MEAN) s_alpha[e] = alpha_i[(int64_t)(n0 + e) * ldc];
+        }
+    };
+    const int nb = (n_end - n_beg) / 32;  // N_pad and the split bounds are multiples of 32
+    __syncthreads();
+    issue_rt(0);
+#pragma unroll 1
+    for (int bg = 0; bg < nb; ++bg) {
+        const int lb = bg % (kGpChunk / 32);  // block within the staged chunk of training rows
+        if (lb == 0) {  // every wave is past the previous block's barrier: s_ta may be overwritten
+            stage_ta(n_beg + 32 * bg, min(kGpChunk, n_end - (n_beg + 32 * bg)));
+        }
+        __syncthreads();  // s_ta and Rt block bg in LDS (the barrier's vmcnt(0) retires the copy)
+        if (bg + 1 < nb) issue_rt(bg + 1);  // into the buffer block bg - 1 used
+        const float* buf = s_rt + (bg & 1) * 32 * kGpCols;
+        const float* tp = s_ta + (lb * 32 + l32) * 2 * A::KSP + half * A::KSP;
+        float af[A::KS];
+#pragma unroll
+        for (int f = 0; f < A::KS; ++f) af[f] = tp[f];
+        f32x16 dd;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dd[r] = 0.0f;
+#pragma unroll
+        for (int f = 0; f < A::KS; ++f) dd = __builtin_amdgcn_mfma_f32_32x32x2f32(af[f], qb[f], dd, 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            // keeps the LDS reads of a group (B values, alphas) from being hoisted over earlier groups
+            // (registers: the kernel stays at 3 waves per SIMD)
+            if constexpr (HAS_MEAN) asm volatile("" ::: "memory");
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 bq = reinterpret_cast<const float4*>(buf)[(8 * g + 4 * half + j) * 32 + l32];
+                const float av = __builtin_amdgcn_exp2f(fminf(dd[4 * g + j], log2s));
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq.x, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq.y, acc[1], 0, 0, 0);
+                acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq.z, acc[2], 0, 0, 0);
+                acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq.w, acc[3], 0, 0, 0);
+                if constexpr (HAS_MEAN) macc = fma((double)av, (double)s_alpha[lb * 32 + 8 * g + 4 * half + j], macc);
+            }
+        }
+        __syncthreads();  // every wave done with buffer bg & 1 and (at a chunk end) with s_ta
+    }
+}
+
 template <int D, int CT, bool SK, bool MEAN>
 __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B, const float* __restrict__ xq,
                                               float* __restrict__ partial, float* __restrict__ meanraw, int n_split,
-                                              float* __restrict__ qraw, float4* s_xt, float* s_tn, float* s_alpha) {
+                                              float* __restrict__ qraw, float4* s_xt, float* s_tn, float* s_alpha,
+                                              float* s_rt) {
     constexpr int DP = (D + 3) / 4 * 4;  // LDS row stride (float4 reads)
     constexpr float kL2E = 1.4426950408889634f;
 
@@ -117,6 +321,13 @@ __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B,
                                (r_rank % kGpCols) / 32;
     const float* alpha_i = m.Rt + (int64_t)i * m.N_pad * ldc + alpha_phys;
     double macc = 0.0;
+    if constexpr (kGpStageRt) {
+        gp_qform_dot_staged<D, SK, has_mean>(m, i, cb, n_beg, n_end, xs2, q0, log2s, alpha_i, xt_i, tn2_i, ldc, half,
+                                             l32, acc, macc, s_xt, s_alpha, s_rt);
+    } else if constexpr (kGpDot) {
+        gp_qform_dot_loop<D, SK, has_mean>(m, i, n_beg, n_end, xs2, q0, log2s, Rt_i, alpha_i, xt_i, tn2_i, ldc,
+                                           half, l32, acc, macc, s_xt, s_alpha);
+    } else
     for (int n0 = n_beg; n0 < n_end; n0 += kGpChunk) {
         const int nch = min(kGpChunk, n_end - n0);  // multiple of 32
         __syncthreads();
@@ -220,15 +431,15 @@ template <int D, int CT, bool SK = false>
 __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
                                                   float* __restrict__ partial, float* __restrict__ meanraw,
                                                   int n_split = 1, float* __restrict__ qraw = nullptr) {
-    constexpr int DP = (D + 3) / 4 * 4;
-    __shared__ float4 s_xt[kGpChunk * DP / 4];
+    __shared__ float4 s_xt[kGpChunk * GpAug<D>::F4];
     __shared__ float s_tn[kGpChunk];
     __shared__ float s_alpha[SK ? 1 : kGpChunk];
+    __shared__ __attribute__((aligned(16))) float s_rt[kGpRtBuf];
     const int mcol = m.r - ((int)(blockIdx.y / (4 / CT)) * kGpCols + 32 * CT * (int)(blockIdx.y % (4 / CT)));
     if (!SK && mcol >= 0 && mcol < 32 * CT)  // uniform: the block holding the mean column
-        gp_qform_body<D, CT, SK, true>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha);
+        gp_qform_body<D, CT, SK, true>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha, s_rt);
     else
-        gp_qform_body<D, CT, SK, false>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha);
+        gp_qform_body<D, CT, SK, false>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha, s_rt);
 }
 
 // Few queries (B <= 8): the posterior is a GEMV per GP, bound by streaming
