@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 10
+#define RCBF_ABI_VERSION 11
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -213,13 +213,17 @@ int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom,
  * exact GP per state dimension i (ScaleKernel(RBF) + Gaussian likelihood,
  * gp_model.py:12-27) on shared normalised training inputs.  Built on the
  * host after each fit (rcbf_amd.gp); all arrays are device memory. */
+#define RCBF_GP_RT_UPPER 1
+
 typedef struct rcbf_gp_model {
     int32_t n_s;     /* GPs = state dims = input dims (3 or 10)                 */
     int32_t N;       /* training points                                         */
     int32_t N_pad;   /* N rounded up to a multiple of 32 (padding rows: Rt = 0)  */
     int32_t r;       /* rank of the variance factor (r = N: exact posterior)     */
     int32_t C_pad;   /* columns of Rt per GP: multiple of 128, >= r + 1          */
-    int32_t _pad;
+    int32_t flags;   /* RCBF_GP_RT_UPPER: logical column j < r of Rt is zero below
+                        row j (R = L^-T of the exact Cholesky factor), so column
+                        block cb reads only training rows < 128 (cb + 1)          */
     const float* xt;       /* (n_s, N_pad, n_s): train_x / (std + 1e-8) / (sqrt2 l_i) */
     const float* tn2;      /* (n_s, N_pad): squared norms of the xt rows             */
     const float* Rt;       /* (n_s, N_pad, C_pad): [R_i | alpha_i | 0], R R^T = (K+nI)^-1;

@@ -11,10 +11,15 @@
 // block of query rows b
 //   Q_i(b, :) = k_i(b, X) Rt_i      -- a (B x N) (N x C) GEMM per GP
 //   var = s_i + n_i - sum_{j<r} Q_i(b,j)^2,   mean = Q_i(b, r)
-// k_i(b, X) is never stored: each wave builds its MFMA A-operand values
-// in registers from the scaled inputs (|xq|^2 + |xt|^2 - 2 xq.xt, then exp),
-// and the GEMM runs on the fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32
-// products, the precision the reference's gpytorch model computes in).
+// k_i(b, X) is never stored.  For every 32 training rows a wave forms the
+// 32 x 32 exponent arguments of its 32 query rows with one small MFMA product
+// over augmented vectors, then one exp2 per lane and k-step gives the A
+// operand of the main product; [R | alpha] is staged once per workgroup in
+// LDS.  Both products run on the fp32 MFMA (v_mfma_f32_32x32x2_f32, exact
+// fp32 products, the precision the reference's gpytorch model computes in).
+// For the exact posterior R = L^-T is upper triangular and the column block
+// of logical columns [128 cb, 128 cb + 128) reads only training rows below
+// 128 (cb + 1): half the work of the dense product (RCBF_GP_RT_UPPER).
 #include "rcbf_common.hpp"
 
 using namespace rcbf;
@@ -28,17 +33,13 @@ constexpr int kGpRows = 128;   // query rows per workgroup
 constexpr int kGpCols = 128;   // Rt columns per workgroup
 constexpr int kGpChunk = 256;  // training rows staged in LDS at a time
 #ifndef RCBF_GP_DOT_MFMA
-#define RCBF_GP_DOT_MFMA 0
+#define RCBF_GP_DOT_MFMA 1
 #endif
-// Distance dot products on the MFMA (see gp_qform_body): per 32 training
-// rows, 32 x 32 arguments from one augmented product of K = D + 2 (padded
-// to even), instead of D VALU FMAs per k-step.
+// 1 (r04, the product): the arguments on the MFMA and [R | alpha] staged in
+// LDS (gp_qform_dot_staged).  0: the earlier loop, kept for A/B builds: D VALU
+// FMAs per A value and every wave loading its own B values.
 constexpr bool kGpDot = RCBF_GP_DOT_MFMA != 0;
-// ... and (level 2) the B operand [R | alpha] staged once per workgroup in
-// LDS by global_load_lds (two 32-row buffers), instead of each wave loading
-// the same rows into its own registers.
-constexpr bool kGpStageRt = RCBF_GP_DOT_MFMA >= 2;
-constexpr int kGpRtBuf = kGpStageRt ? 2 * 32 * kGpCols : 1;  // floats
+constexpr int kGpRtBuf = kGpDot ? 2 * 32 * kGpCols : 1;  // floats: two 32-row slices of the column block
 template <int D>
 struct GpAug {
     static constexpr int KA = (D + 2 + 1) / 2 * 2;    // [q0 | 1 | 2 L2E xs] . [1 | tn | xt], padded to even
@@ -47,29 +48,6 @@ struct GpAug {
     static constexpr int F4 = kGpDot ? 2 * KSP / 4 : (D + 3) / 4;  // float4s per staged training row
 };
 
-// Workgroup (row tile of 128 queries, column block cb of 128, GP i): wave w
-// owns query rows 32w..32w+31 and all 128 columns (4 tiles of 32 x 32), so
-// every A-operand value k_i(x_b, x_n) is built exactly once per workgroup and
-// each wave reduces its own rows (no cross-wave combine).  Per k-step of 2
-// training points a wave builds 1 A value per lane (10 fma + exp2) and
-// issues 4 MFMAs; the B values of the next 4 k-steps are loaded while the
-// current ones are consumed (register double buffer).
-// partial[(i * n_cb + cb) * B + b] = sum over this block's columns j < r of Q^2;
-// meanraw[i * B + b] = Q(b, r) from the block holding column r.
-// Split-K (SK, small grids: few query tiles or a low-rank [R | alpha]):
-// blockIdx.z = i * n_split + s and the workgroup sums only training rows
-// [s per, (s + 1) per); it stores its raw Q tile to
-// qraw[((i * n_split + s) * B + b) * C_pad + col] and k_gp_combine adds the
-// n_split tiles (fixed order, deterministic) before squaring.
-// The mean column (logical column r) of the single pass is not taken from
-// the fp32 MFMA accumulator (one running sum over all N training rows: the
-// large alternating alpha of an ill-conditioned fit made that chain lose
-// 3e-4 of max|mean|).  Each lane instead adds its own A value times alpha_n
-// (staged in LDS with the chunk) into an fp64 sum -- the products of two
-// fp32 values are exact in fp64 -- and the two half-waves' sums are added in
-// the epilogue.  One v_fma_f64 per k-step beside four MFMAs.
-// MEAN: this workgroup's column block holds the mean column r (a separate
-// instantiation, so the other ~95 % of the workgroups run the plain loop).
 // This lane's B operand of the dot product: element 2 f + half of
 // [q0, 1, 2 L2E xs, 0...].  The values pass through an empty asm first, so the
 // half-select stays a select of two registers (folded into a select of two
@@ -88,89 +66,17 @@ __device__ __forceinline__ void gp_query_operand(const float (&xs2)[D], float q0
     for (int f = 0; f < A::KS; ++f) qb[f] = half ? qa[2 * f + 1] : qa[2 * f];
 }
 
-// The training loop with the distance dot products on the MFMA (kGpDot).
-// Per block of 32 training rows t and the wave's 32 query rows b, one
-// v_mfma_f32_32x32x2_f32 product over the augmented vectors
+// The training loop (kGpDot).  Per block of 32 training rows t and the
+// wave's 32 query rows b, one v_mfma_f32_32x32x2_f32 product over
 //   arg(t, b) = [1, tn_t, xt_t] . [q0_b, 1, 2 L2E xs_b]
-// (K = D + 2, padded to even; KS k-steps) leaves arg(t, b) in the C layout:
-// lane l, register r holds t = (r & 3) + 8 (r >> 2) + 4 (l >> 5), b = l & 31.
-// That is exactly the A-operand layout of the main product's k-step r (query
-// l & 31, training row t for the lane's half), so each k-step costs one
-// fminf + exp2 per lane (the A value) beside its 4 MFMAs, and the B operand
-// of k-step r is Rt row t -- rows 8 g + 4 half + j of the block in group g =
-// r >> 2, j = r & 3.  The augmented order (q0 + tn first, then the D
-// products) is the order of the VALU chain it replaces.
-template <int D, bool SK, bool HAS_MEAN>
-__device__ __forceinline__ void gp_qform_dot_loop(const rcbf_gp_model& m, int i, int n_beg, int n_end,
-                                                  const float (&xs2)[D], float q0, float log2s, const float* Rt_i,
-                                                  const float* alpha_i, const float* xt_i, const float* tn2_i,
-                                                  int64_t ldc, int half, int l32, f32x16* acc, double& macc,
-                                                  float4* s_xt, float* s_alpha) {
-    using A = GpAug<D>;
-    constexpr float kL2E = 1.4426950408889634f;
-    float* s_ta = reinterpret_cast<float*>(s_xt);
-    // this lane's B operand of the dot product: element 2 f + half of [q0, 1, 2 L2E xs, 0...]
-    float qb[A::KS];
-    gp_query_operand<D>(xs2, q0, half, qb);
-    const float* rp = Rt_i + (int64_t)(n_beg + 4 * half) * ldc;  // row 8 gi + j of the range, this half
-    // one 4-deep ring of B values per k-step slot j = r & 3: k-step r's slot
-    // is refilled with k-step r + 4's row right after its MFMAs issue
-    float bv[4][4];
-    auto ldb = [&](int64_t row, float* dst) {
-        const float4 v = *reinterpret_cast<const float4*>(rp + row * ldc);
-        dst[0] = v.x, dst[1] = v.y, dst[2] = v.z, dst[3] = v.w;
-    };
-    for (int n0 = n_beg; n0 < n_end; n0 += kGpChunk) {
-        const int nch = min(kGpChunk, n_end - n0);  // multiple of 32
-        __syncthreads();
-        for (int e = threadIdx.x; e < nch; e += 256) {
-            float ta[A::KA];
-            ta[0] = 1.0f;
-            ta[1] = -kL2E * tn2_i[n0 + e];
-#pragma unroll
-            for (int k = 0; k < A::KA - 2; ++k) ta[2 + k] = k < D ? xt_i[(int64_t)(n0 + e) * D + k] : 0.0f;
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int f = 0; f < A::KSP; ++f) s_ta[e * 2 * A::KSP + h * A::KSP + f] = f < A::KS ? ta[2 * f + h] : 0.0f;
-            if constexpr (HAS_MEAN) s_alpha[e] = alpha_i[(int64_t)(n0 + e) * ldc];
-        }
-        __syncthreads();
-        const int64_t base = n0 - n_beg;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ldb(base + j, bv[j]);
-        const int nblk = nch / 32;
-#pragma unroll 1
-        for (int blk = 0; blk < nblk; ++blk) {
-            const float* tp = s_ta + (blk * 32 + l32) * 2 * A::KSP + half * A::KSP;
-            float af[A::KS];
-#pragma unroll
-            for (int f = 0; f < A::KS; ++f) af[f] = tp[f];
-            f32x16 dd;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) dd[r] = 0.0f;
-#pragma unroll
-            for (int f = 0; f < A::KS; ++f) dd = __builtin_amdgcn_mfma_f32_32x32x2f32(af[f], qb[f], dd, 0, 0, 0);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                // the group of k-step r + 4 in this chunk; past the chunk's end the ring reloads the
-                // chunk's last group (branch-free; the values are not used)
-                const int gn = min(blk * 4 + g + 1, nblk * 4 - 1);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float av = __builtin_amdgcn_exp2f(fminf(dd[4 * g + j], log2s));
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-                        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[j][c], acc[c], 0, 0, 0);
-                    if constexpr (HAS_MEAN) macc = fma((double)av, (double)s_alpha[blk * 32 + 8 * g + 4 * half + j], macc);
-                    ldb(base + 8 * gn + j, bv[j]);
-                }
-            }
-        }
-    }
-}
-
-// Level 2 of gp_qform_dot_loop: block bg's 32 x 128 slice of Rt (16 KB) is
+// (K = D + 2, padded to even: KS k-steps; q0 + tn first, then the D
+// products, the order of the VALU chain it replaces) leaves arg(t, b) in the
+// C layout: lane l, register r holds t = (r & 3) + 8 (r >> 2) + 4 (l >> 5),
+// b = l & 31 -- exactly the A-operand layout of the main product's k-step r,
+// so each k-step costs one fminf + exp2 per lane beside its 4 MFMAs, and the
+// B operand of k-step r is Rt row t: rows 8 g + 4 half + j of the block in
+// group g = r >> 2, j = r & 3.
+// Block bg's 32 x 128 slice of Rt (16 KB) is
 // copied to LDS buffer bg & 1 by the whole workgroup with 4 global_load_lds
 // (16 B per lane, lane-linear: one wave-instruction = 2 rows) while block
 // bg - 1 is computed; one barrier per block.  The k-step r B value of lane
@@ -214,16 +120,18 @@ __device__ __forceinline__ void gp_qform_dot_staged(const rcbf_gp_model& m, int 
         }
     };
     const int nb = (n_end - n_beg) / 32;  // N_pad and the split bounds are multiples of 32
-    __syncthreads();
-    issue_rt(0);
+    if (nb > 0) issue_rt(0);
 #pragma unroll 1
     for (int bg = 0; bg < nb; ++bg) {
         const int lb = bg % (kGpChunk / 32);  // block within the staged chunk of training rows
-        if (lb == 0) {  // every wave is past the previous block's barrier: s_ta may be overwritten
+        if (lb == 0) {  // a new chunk of training rows: every wave done with the previous one first
+            __syncthreads();
             stage_ta(n_beg + 32 * bg, min(kGpChunk, n_end - (n_beg + 32 * bg)));
         }
-        __syncthreads();  // s_ta and Rt block bg in LDS (the barrier's vmcnt(0) retires the copy)
-        if (bg + 1 < nb) issue_rt(bg + 1);  // into the buffer block bg - 1 used
+        // ONE barrier per block: its vmcnt(0) retires this wave's copy of block bg, and past it every
+        // wave has finished block bg - 1, so its buffer ((bg + 1) & 1) is free for block bg + 1
+        __syncthreads();
+        if (bg + 1 < nb) issue_rt(bg + 1);
         const float* buf = s_rt + (bg & 1) * 32 * kGpCols;
         const float* tp = s_ta + (lb * 32 + l32) * 2 * A::KSP + half * A::KSP;
         float af[A::KS];
@@ -250,10 +158,32 @@ __device__ __forceinline__ void gp_qform_dot_staged(const rcbf_gp_model& m, int 
                 if constexpr (HAS_MEAN) macc = fma((double)av, (double)s_alpha[lb * 32 + 8 * g + 4 * half + j], macc);
             }
         }
-        __syncthreads();  // every wave done with buffer bg & 1 and (at a chunk end) with s_ta
     }
 }
 
+// Workgroup (row tile of 128 queries, column block cb of 128, GP i): wave w
+// owns query rows 32w..32w+31 and all 128 columns (4 tiles of 32 x 32), so
+// every A-operand value k_i(x_b, x_n) is built exactly once per workgroup and
+// each wave reduces its own rows (no cross-wave combine).  Per k-step of 2
+// training points a wave issues 4 MFMAs with one A value per lane
+// (gp_qform_dot_staged; the level-0 loop builds it from D VALU FMAs + exp2
+// and loads its own B values 4 k-steps ahead).
+// partial[(i * n_cb + cb) * B + b] = sum over this block's columns j < r of Q^2;
+// meanraw[i * B + b] = Q(b, r) from the block holding column r.
+// Split-K (SK, small grids: few query tiles or a low-rank [R | alpha]):
+// blockIdx.z = i * n_split + s and the workgroup sums only training rows
+// [s per, (s + 1) per); it stores its raw Q tile to
+// qraw[((i * n_split + s) * B + b) * C_pad + col] and k_gp_combine adds the
+// n_split tiles (fixed order, deterministic) before squaring.
+// The mean column (logical column r) of the single pass is not taken from
+// the fp32 MFMA accumulator (one running sum over all N training rows: the
+// large alternating alpha of an ill-conditioned fit made that chain lose
+// 3e-4 of max|mean|).  Each lane instead adds its own A value times alpha_n
+// (staged in LDS with the training rows) into an fp64 sum -- the products of two
+// fp32 values are exact in fp64 -- and the two half-waves' sums are added in
+// the epilogue.  One v_fma_f64 per k-step beside four MFMAs.
+// MEAN: this workgroup's column block holds the mean column r (a separate
+// instantiation, so the other ~95 % of the workgroups run the plain loop).
 template <int D, int CT, bool SK, bool MEAN>
 __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B, const float* __restrict__ xq,
                                               float* __restrict__ partial, float* __restrict__ meanraw, int n_split,
@@ -311,6 +241,11 @@ __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B,
         n_beg = min(m.N_pad, split * per);
         n_end = min(m.N_pad, n_beg + per);
     }
+    // exact posterior: R = L^-T, so logical column j has no nonzero row past j and this block's columns
+    // (< 128 (cb + 1)) read only the training rows below that (the alpha column r = N sits in the last
+    // block, whose bound is >= N_pad).  Half the MFMA work and the Rt traffic of the dense product.
+    if (m.flags & RCBF_GP_RT_UPPER) n_end = min(n_end, (cb + 1) * kGpCols);
+    n_end = max(n_end, n_beg);  // an empty split (SK): the workgroup stores a zero tile
     // does this workgroup hold the mean column r (uniform)?  alpha_n = Rt[n][r] sits at the physical
     // column of logical column r (128-column blocks, lane-interleaved: 4 l + c holds 32 c + l)
     const int r_rank = m.r;
@@ -321,12 +256,9 @@ __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B,
                                (r_rank % kGpCols) / 32;
     const float* alpha_i = m.Rt + (int64_t)i * m.N_pad * ldc + alpha_phys;
     double macc = 0.0;
-    if constexpr (kGpStageRt) {
+    if constexpr (kGpDot) {
         gp_qform_dot_staged<D, SK, has_mean>(m, i, cb, n_beg, n_end, xs2, q0, log2s, alpha_i, xt_i, tn2_i, ldc, half,
                                              l32, acc, macc, s_xt, s_alpha, s_rt);
-    } else if constexpr (kGpDot) {
-        gp_qform_dot_loop<D, SK, has_mean>(m, i, n_beg, n_end, xs2, q0, log2s, Rt_i, alpha_i, xt_i, tn2_i, ldc,
-                                           half, l32, acc, macc, s_xt, s_alpha);
     } else
     for (int n0 = n_beg; n0 < n_end; n0 += kGpChunk) {
         const int nch = min(kGpChunk, n_end - n0);  // multiple of 32
@@ -465,7 +397,10 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
     const float sl = m.inv_sl[i];
     const float log2s = __log2f(m.outscale[i]);
     const int n0 = rs * kGvRows;
-    {
+    // exact posterior (upper-triangular R): this column chunk's logical columns are < 256 (cc + 1), so a
+    // row split at or past that is all zero -- the workgroup only stores its zero partial sums
+    const bool zero_tile = (m.flags & RCBF_GP_RT_UPPER) && n0 >= (cc + 1) * kGvCols;
+    if (!zero_tile) {
         const int n = n0 + t;
         const bool in = n < m.N_pad;
         float xt[D];
@@ -496,7 +431,7 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
 #pragma unroll
     for (int b = 0; b < BQ; ++b) acc[b] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const int nr = min(64, m.N_pad - (n0 + 64 * w));  // rows of this wave (N_pad is a multiple of 32)
-    if (colin && nr > 0) {
+    if (colin && nr > 0 && !zero_tile) {
         const float* R = m.Rt + ((int64_t)i * m.N_pad + n0 + 64 * w) * ldc + pcol;
         const float* kw = &s_k[0][64 * w];
         if (nr == 64) {

@@ -23,7 +23,7 @@ SOLVER_PDIPM = 1
 SOLVER_GI = 2
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NONFINITE = 0, 1, 2, 3
 MAX_HAZARDS = 8
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL"}
 
@@ -57,10 +57,13 @@ _U64 = ctypes.c_uint64
 _PRM = ctypes.POINTER(RcbfParams)
 
 
+GP_RT_UPPER = 1  # rcbf_gp_model.flags: [R | alpha] upper triangular (exact posterior)
+
+
 class RcbfGpModel(ctypes.Structure):
     """include/rcbf_hip.h rcbf_gp_model (device pointers as integers)."""
     _fields_ = [("n_s", ctypes.c_int32), ("N", ctypes.c_int32), ("N_pad", ctypes.c_int32), ("r", ctypes.c_int32),
-                ("C_pad", ctypes.c_int32), ("_pad", ctypes.c_int32),
+                ("C_pad", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("xt", ctypes.c_void_p), ("tn2", ctypes.c_void_p), ("Rt", ctypes.c_void_p),
                 ("x_std", ctypes.c_void_p), ("inv_sl", ctypes.c_void_p), ("outscale", ctypes.c_void_p),
                 ("noise", ctypes.c_void_p), ("y_scale", ctypes.c_void_p)]

@@ -120,7 +120,9 @@ class GPDisturbanceModel:
         self.outscale = torch.tensor([h[1] for h in self.hyper], dtype=torch.float32, device=dev)
         self.noise = torch.tensor([h[2] for h in self.hyper], dtype=torch.float32, device=dev)
         self.y_scale = torch.as_tensor(y_std + 1e-8, dtype=torch.float32, device=dev)
-        self._m = _lib.RcbfGpModel(n_s, N, N_pad, self.r, C_pad, 0, *(t.data_ptr() for t in (
+        # exact: R = L^-T is upper triangular, so the kernels skip the zero rows of each column block
+        flags = _lib.GP_RT_UPPER if self.r == N else 0
+        self._m = _lib.RcbfGpModel(n_s, N, N_pad, self.r, C_pad, flags, *(t.data_ptr() for t in (
             self.xt, self.tn2, self.Rt, self.x_std, self.inv_sl, self.outscale, self.noise, self.y_scale)))
         self._ws = torch.empty(0, dtype=torch.float32, device=dev)
 
@@ -169,7 +171,14 @@ class GPDisturbanceModel:
         return (mc, sc, mr, sr) if rows else (mc, sc)
 
     def flops_per_query(self):
-        """Algorithmic MFMA flops per query row: 2 N C_pad per GP."""
+        """Algorithmic MFMA flops per query row of the k(x, X) [R | alpha]
+        product: 2 N C_pad per GP dense; with the upper-triangular factor
+        (exact posterior) column block cb only meets training rows below
+        128 (cb + 1), so 2 * 128 * sum_cb min(N, 128 (cb + 1)) per GP."""
+        n_cb = self._m.C_pad // _PAD_C
+        if self._m.flags & _lib.GP_RT_UPPER:
+            k = sum(min(self.N, _PAD_C * (cb + 1)) for cb in range(n_cb))
+            return 2 * _PAD_C * k * self.n_s
         return 2 * self.N * self._m.C_pad * self.n_s
 
 

@@ -21,6 +21,8 @@ rng = np.random.default_rng(0)
 tx = rng.normal(0, 1, (N, n_s))
 ty = 0.1 * np.sin(tx) + rng.normal(0, 0.05, (N, n_s))
 model = gp.GPDisturbanceModel(tx, ty, [(1.5, 0.2, 0.05)] * n_s)
+if os.environ.get("RCBF_GP_DENSE"):  # A/B: read the whole [R | alpha] (no upper-triangular skip)
+    model._m.flags = 0
 x = torch.as_tensor(rng.normal(0, 1, (B, n_s)), dtype=torch.float32, device="cuda")
 for _ in range(2):
     model.predict(x)

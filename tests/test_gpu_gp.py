@@ -136,6 +136,27 @@ def test_gp_split_k_matches_single_pass():
     assert np.max(np.abs(s_1.cpu().numpy() - so[:1]) / so[:1]) <= 1e-4
 
 
+@pytest.mark.parametrize("B", [1, 5, 256, 1000, 4096])
+def test_gp_upper_triangular_skip_is_exact(B):
+    """The exact posterior's factor R = L^-T is upper triangular, so the
+    kernels skip the training rows past each column block (rcbf_gp_model
+    flags RCBF_GP_RT_UPPER): the skipped terms are exact zeros, so the outputs
+    equal the dense product's bit for bit (GEMV path B <= 8, split-K, single
+    pass)."""
+    from rcbf_amd import _lib, gp
+    rng = np.random.default_rng(B)
+    tx, ty = _data(rng, 1100, 10)
+    model = gp.GPDisturbanceModel(tx, ty, [(1.3, 0.2, 0.05)] * 10)
+    assert model._m.flags == _lib.GP_RT_UPPER
+    lR = model.logical_Rt()[:, :, :model.r].cpu().numpy()
+    assert not np.any(np.tril(np.ones(lR.shape[1:], bool), -1)[None] & (lR != 0))  # zero below the diagonal
+    q = torch.as_tensor((rng.normal(0, 1, (B, 10)) * tx.std(0)).astype(np.float32), device="cuda")
+    m_t, s_t = model.predict(q)
+    model._m.flags = 0
+    m_d, s_d = model.predict(q)
+    assert torch.equal(m_t, m_d) and torch.equal(s_t, s_d)
+
+
 def test_gp_predict_low_rank_split_k():
     """rank 100 (the root-decomposition size of gpytorch's fast_pred_var,
     gp_model.py:97): one 128-column block per GP, so B = 256 runs split-K."""
