@@ -235,17 +235,16 @@ __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B,
     // its B values for the 4 column tiles.
     const float* Rt_i = m.Rt + (int64_t)i * m.N_pad * ldc + (int64_t)cb * kGpCols + 4 * l32 + CT * sub;
 
-    int n_beg = 0, n_end = m.N_pad;
-    if constexpr (SK) {
-        const int per = ((m.N_pad + n_split - 1) / n_split + 31) / 32 * 32;
-        n_beg = min(m.N_pad, split * per);
-        n_end = min(m.N_pad, n_beg + per);
-    }
     // exact posterior: R = L^-T, so logical column j has no nonzero row past j and this block's columns
     // (< 128 (cb + 1)) read only the training rows below that (the alpha column r = N sits in the last
     // block, whose bound is >= N_pad).  Half the MFMA work and the Rt traffic of the dense product.
-    if (m.flags & RCBF_GP_RT_UPPER) n_end = min(n_end, (cb + 1) * kGpCols);
-    n_end = max(n_end, n_beg);  // an empty split (SK): the workgroup stores a zero tile
+    const int k_end = (m.flags & RCBF_GP_RT_UPPER) ? min(m.N_pad, (cb + 1) * kGpCols) : m.N_pad;
+    int n_beg = 0, n_end = k_end;
+    if constexpr (SK) {  // this block's rows in n_split equal parts (multiples of 32)
+        const int per = ((k_end + n_split - 1) / n_split + 31) / 32 * 32;
+        n_beg = min(k_end, split * per);
+        n_end = min(k_end, n_beg + per);
+    }
     // does this workgroup hold the mean column r (uniform)?  alpha_n = Rt[n][r] sits at the physical
     // column of logical column r (128-column blocks, lane-interleaved: 4 l + c holds 32 c + l)
     const int r_rank = m.r;
@@ -388,19 +387,23 @@ constexpr int kGvCols = 256;  // physical Rt columns per workgroup (4 per lane)
 
 template <int D, int BQ>
 __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
-                                                 int n_rs, float* __restrict__ qraw) {
+                                                 int n_rs, float* __restrict__ qraw, int tri) {
     constexpr float kL2E = 1.4426950408889634f;
     __shared__ float s_k[BQ][kGvRows];
     __shared__ float4 s_red[3][BQ][64];
-    const int cc = blockIdx.x, rs = blockIdx.y, i = blockIdx.z;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int i = blockIdx.z;
+    int cc = blockIdx.x, rs = blockIdx.y;
+    if (tri) {  // exact posterior: only the tiles rs <= cc hold nonzero rows; blockIdx.x enumerates them, cc-major
+        int tt = blockIdx.x;
+        cc = 0;
+        while (tt >= min(n_rs, cc + 1)) tt -= min(n_rs, cc + 1), ++cc;
+        rs = tt;
+    }
     const float sl = m.inv_sl[i];
     const float log2s = __log2f(m.outscale[i]);
     const int n0 = rs * kGvRows;
-    // exact posterior (upper-triangular R): this column chunk's logical columns are < 256 (cc + 1), so a
-    // row split at or past that is all zero -- the workgroup only stores its zero partial sums
-    const bool zero_tile = (m.flags & RCBF_GP_RT_UPPER) && n0 >= (cc + 1) * kGvCols;
-    if (!zero_tile) {
+    {
         const int n = n0 + t;
         const bool in = n < m.N_pad;
         float xt[D];
@@ -431,7 +434,7 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
 #pragma unroll
     for (int b = 0; b < BQ; ++b) acc[b] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const int nr = min(64, m.N_pad - (n0 + 64 * w));  // rows of this wave (N_pad is a multiple of 32)
-    if (colin && nr > 0 && !zero_tile) {
+    if (colin && nr > 0) {
         const float* R = m.Rt + ((int64_t)i * m.N_pad + n0 + 64 * w) * ldc + pcol;
         const float* kw = &s_k[0][64 * w];
         if (nr == 64) {
@@ -490,9 +493,11 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
 // Split-K combine: one wave per (GP i, column block cb, query b) adds the
 // n_split raw Q rows (fixed order) over the block's 128 columns, then
 // partial = sum_{col < r} Q^2 and meanraw = Q(b, r), as k_gp_qform's own epilogue.
+// tri (the GEMV path on an upper-triangular factor): row split s of column chunk
+// col / 256 was not launched when its rows start at or past 256 (chunk + 1).
 __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, int n_cb, int n_split,
                                                     const float* __restrict__ qraw, float* __restrict__ partial,
-                                                    float* __restrict__ meanraw) {
+                                                    float* __restrict__ meanraw, int tri) {
     const int64_t wv = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wv >= (int64_t)m.n_s * n_cb * B) return;
@@ -505,7 +510,8 @@ __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, 
     for (int h = 0; h < 2; ++h) {
         const int col = cb * kGpCols + 64 * h + lane;  // logical column: k_gp_qform stores Q by logical column
         float q = 0.0f;
-        for (int s = 0; s < n_split; ++s) q += qraw[(((int64_t)i * n_split + s) * B + b) * ldc + col];
+        const int ns = tri ? min(n_split, col / kGvCols + 1) : n_split;
+        for (int s = 0; s < ns; ++s) q += qraw[(((int64_t)i * n_split + s) * B + b) * ldc + col];
         v += (col < m.r) ? q * q : 0.0f;
         if (col == m.r) meanraw[(int64_t)i * B + b] = q;
     }
@@ -569,6 +575,9 @@ constexpr int kGvMaxB = 8;  // B <= 8: the streaming GEMV path
 
 int gp_split(const rcbf_gp_model* m, int64_t B) {
     if (B <= kGvMaxB) return (m->N_pad + kGvRows - 1) / kGvRows;  // GEMV row splits
+#ifdef RCBF_STUDY_GP_SPLIT  // study builds only: the split count from the environment
+    if (const char* e = getenv("RCBF_GP_SPLIT")) return atoi(e) < 1 ? 1 : atoi(e);
+#endif
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
@@ -628,9 +637,14 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
     float* meanraw = workspace + (int64_t)m->n_s * 2 * n_cb * B;
     const int sk = gp_split(m, B);
     float* qraw = meanraw + (int64_t)m->n_s * B;
+    const bool tri = (m->flags & RCBF_GP_RT_UPPER) != 0;
     if (B <= kGvMaxB) {
-        dim3 gv((unsigned)((m->C_pad + kGvCols - 1) / kGvCols), (unsigned)sk, (unsigned)m->n_s);
-#define RCBF_GV_L(DD, BB) hipLaunchKernelGGL((k_gp_gemv<DD, BB>), gv, dim3(256), 0, stream, *m, B, x, sk, qraw)
+        const int n_cc = (m->C_pad + kGvCols - 1) / kGvCols;
+        int tiles = 0;  // upper-triangular factor: only the tiles rs <= cc (k_gp_gemv decodes them)
+        for (int c = 0; c < n_cc; ++c) tiles += sk < c + 1 ? sk : c + 1;
+        dim3 gv(tri ? (unsigned)tiles : (unsigned)n_cc, tri ? 1u : (unsigned)sk, (unsigned)m->n_s);
+#define RCBF_GV_L(DD, BB) \
+    hipLaunchKernelGGL((k_gp_gemv<DD, BB>), gv, dim3(256), 0, stream, *m, B, x, sk, qraw, (int)tri)
 #define RCBF_GV_B(DD)           \
     do {                        \
         if (B == 1)             \
@@ -680,7 +694,7 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
     if (sk > 1 || B <= kGvMaxB) {
         const int64_t waves = (int64_t)m->n_s * n_cb * B;
         hipLaunchKernelGGL(k_gp_combine, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, *m, B, n_cb, sk,
-                           qraw, partial, meanraw);
+                           qraw, partial, meanraw, (int)(tri && B <= kGvMaxB));
     }
     if (mean_out || std_out) {
         const int64_t tot = B * m->n_s;

@@ -140,9 +140,10 @@ def test_gp_split_k_matches_single_pass():
 def test_gp_upper_triangular_skip_is_exact(B):
     """The exact posterior's factor R = L^-T is upper triangular, so the
     kernels skip the training rows past each column block (rcbf_gp_model
-    flags RCBF_GP_RT_UPPER): the skipped terms are exact zeros, so the outputs
-    equal the dense product's bit for bit (GEMV path B <= 8, split-K, single
-    pass)."""
+    flags RCBF_GP_RT_UPPER): the skipped terms are exact zeros, so the single
+    pass (B = 4096) and the GEMV path (B <= 8) equal the dense product's
+    outputs bit for bit.  Split-K (B = 256, 1000) splits each block's own row
+    range evenly, so its fp32 partial sums group differently: within 1e-6."""
     from rcbf_amd import _lib, gp
     rng = np.random.default_rng(B)
     tx, ty = _data(rng, 1100, 10)
@@ -154,7 +155,11 @@ def test_gp_upper_triangular_skip_is_exact(B):
     m_t, s_t = model.predict(q)
     model._m.flags = 0
     m_d, s_d = model.predict(q)
-    assert torch.equal(m_t, m_d) and torch.equal(s_t, s_d)
+    if B in (256, 1000):
+        assert torch.allclose(m_t, m_d, rtol=1e-6, atol=1e-6 * m_d.abs().max().item())
+        assert torch.allclose(s_t, s_d, rtol=1e-6, atol=0)
+    else:
+        assert torch.equal(m_t, m_d) and torch.equal(s_t, s_d)
 
 
 def test_gp_predict_low_rank_split_k():
