@@ -92,20 +92,22 @@ __global__ void __launch_bounds__(kBlock) k_model_step(rcbf_params prm, int64_t 
     if (z) {
 #pragma unroll
         for (int k = 0; k < NS; ++k) zz[k] = z[i * NS + k];
-    } else {  // N(0,1) pairs from Philox4x32-10 keyed by (seed, row, counter, pair)
+    } else {  // N(0,1) from Philox4x32-10 keyed by (seed, row, counter, call q): one call = 4 words = 2
+              // Box-Muller pairs on 24-bit uniforms with the hardware fp32 log2 / sin / cos (as the envs'
+              // reset draw, normal_draw); statistically N(0, 1), |z| <= 5.8 (r04: cars 5 fp64 pairs -> 3 calls)
 #pragma unroll
-        for (int p = 0; p < (NS + 1) / 2; ++p) {
-            uint32_t cc[4] = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), (uint32_t)counter, (uint32_t)p};
+        for (int q = 0; q < (NS + 3) / 4; ++q) {
+            uint32_t cc[4] = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), (uint32_t)counter, (uint32_t)q};
             philox4x32_10(cc, (uint32_t)seed, (uint32_t)(seed >> 32));
-            const double u1 = ((double)((((uint64_t)cc[0] << 21) ^ cc[1]) & ((1ull << 53) - 1)) + 1.0) *
-                              (1.0 / 9007199254740992.0);
-            const double u2 = (double)((((uint64_t)cc[2] << 21) ^ cc[3]) & ((1ull << 53) - 1)) *
-                              (1.0 / 9007199254740992.0);
-            const double r = sqrt(-2.0 * log(u1));
-            double sn, cs;
-            sincospi(2.0 * u2, &sn, &cs);
-            zz[2 * p] = r * cs;
-            if (2 * p + 1 < NS) zz[2 * p + 1] = r * sn;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float f1 = ((float)(cc[2 * h] >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+                const float f2 = (float)(cc[2 * h + 1] >> 8) * (1.0f / 16777216.0f);      // [0, 1) revolutions
+                const float r = __builtin_sqrtf(-2.0f * __builtin_amdgcn_logf(f1) * 0.69314718f);
+                const int k = 4 * q + 2 * h;
+                if (k < NS) zz[k] = (double)(r * __builtin_amdgcn_cosf(f2));
+                if (k + 1 < NS) zz[k + 1] = (double)(r * __builtin_amdgcn_sinf(f2));
+            }
         }
     }
     double ns[NS];
