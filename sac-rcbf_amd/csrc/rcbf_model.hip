@@ -124,7 +124,8 @@ __global__ void __launch_bounds__(kBlock) k_model_step(rcbf_params prm, int64_t 
     const double tn = ti + dt;
     if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
 #pragma unroll
-        for (int k = 0; k < 10; ++k) next_obs[i * NO + k] = ns[k] / ((k & 1) ? 30.0 : 100.0);
+        for (int k = 0; k < 10; ++k)  // correctly rounded x / d in 3 FMAs (div_const), numpy's x / d bit for bit
+            next_obs[i * NO + k] = (k & 1) ? div_const(ns[k], 30.0, 1.0 / 30.0) : div_const(ns[k], 100.0, 1.0 / 100.0);
         r = -5.0 * fabs(u[0] * u[0]) / 300.0;     // generate_rollouts.py:62
         msk = (tn >= 300.0 * 0.02) ? 0.0 : 1.0;   // :65-66
     } else {
