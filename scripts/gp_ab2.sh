@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # GP posterior: the GP tests on the product, then 3 interleaved timing rounds of
-#   base  = level-0 kernel (build/variants/librcbf_gpl0.so), dense [R | alpha]
+#   base  = the level-0 kernel (build/variants/librcbf_gpl0.so: python __graft_entry__.py variant gpl0 -DRCBF_GP_DOT_MFMA=0), dense [R | alpha]
 #   dense = the product kernel, dense [R | alpha] (RCBF_GP_DENSE=1)
 #   tri   = the product kernel with the upper-triangular skip
 # at B = 1, 256, 4096 (scripts/gp_one.py).  Usage: bash scripts/gp_ab2.sh TAG
