@@ -32,6 +32,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kGpRows = 128;   // query rows per workgroup
 constexpr int kGpCols = 128;   // Rt columns per workgroup
 constexpr int kGpChunk = 256;  // training rows staged in LDS at a time
+#ifndef RCBF_GP_SK_CHUNK
+#define RCBF_GP_SK_CHUNK 256
+#endif
+// the split-K instantiation (small batches) stages fewer training rows at a time when
+// RCBF_GP_SK_CHUNK < 256, so 4 workgroups fit a CU's LDS (study knob)
+template <bool SK>
+constexpr int gp_chunk() { return SK ? RCBF_GP_SK_CHUNK : kGpChunk; }
 #ifndef RCBF_GP_DOT_MFMA
 #define RCBF_GP_DOT_MFMA 1
 #endif
@@ -123,10 +130,10 @@ __device__ __forceinline__ void gp_qform_dot_staged(const rcbf_gp_model& m, int 
     if (nb > 0) issue_rt(0);
 #pragma unroll 1
     for (int bg = 0; bg < nb; ++bg) {
-        const int lb = bg % (kGpChunk / 32);  // block within the staged chunk of training rows
+        const int lb = bg % (gp_chunk<SK>() / 32);  // block within the staged chunk of training rows
         if (lb == 0) {  // a new chunk of training rows: every wave done with the previous one first
             __syncthreads();
-            stage_ta(n_beg + 32 * bg, min(kGpChunk, n_end - (n_beg + 32 * bg)));
+            stage_ta(n_beg + 32 * bg, min(gp_chunk<SK>(), n_end - (n_beg + 32 * bg)));
         }
         // ONE barrier per block: its vmcnt(0) retires this wave's copy of block bg, and past it every
         // wave has finished block bg - 1, so its buffer ((bg + 1) & 1) is free for block bg + 1
@@ -362,8 +369,8 @@ template <int D, int CT, bool SK = false>
 __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
                                                   float* __restrict__ partial, float* __restrict__ meanraw,
                                                   int n_split = 1, float* __restrict__ qraw = nullptr) {
-    __shared__ float4 s_xt[kGpChunk * GpAug<D>::F4];
-    __shared__ float s_tn[kGpChunk];
+    __shared__ float4 s_xt[(kGpDot ? gp_chunk<SK>() : kGpChunk) * GpAug<D>::F4];
+    __shared__ float s_tn[kGpDot ? 1 : kGpChunk];
     __shared__ float s_alpha[SK ? 1 : kGpChunk];
     __shared__ __attribute__((aligned(16))) float s_rt[kGpRtBuf];
     const int mcol = m.r - ((int)(blockIdx.y / (4 / CT)) * kGpCols + 32 * CT * (int)(blockIdx.y % (4 / CT)));
