@@ -196,3 +196,26 @@ def test_fast_binding_follows_the_library_override(tmp_path):
     env = dict(os.environ, RCBF_HIP_LIB=str(variant))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def _header_struct_fields(name):
+    """Field names of `typedef struct name { ... } name;` in include/rcbf_hip.h, in order."""
+    import re
+    src = open(os.path.join(ROOT, "include", "rcbf_hip.h")).read()
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), src, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = []
+    for decl in (d.strip() for d in body.split(";") if d.strip()):  # "double kp, k_brake" declares two
+        first, *more = decl.split(",")
+        names.append(re.match(r"[\w\s\*]+?[\s\*](\w+)\s*(\[.*\])?$", first.strip()).group(1))
+        names += [re.match(r"\**\s*(\w+)", m.strip()).group(1) for m in more]
+    return names
+
+
+@pytest.mark.parametrize("cname,pyname", [("rcbf_params", "RcbfParams"), ("rcbf_gp_model", "RcbfGpModel")])
+def test_ctypes_mirrors_follow_the_header(cname, pyname):
+    """The ctypes mirrors in rcbf_amd._lib name the header's fields in the
+    header's order (e.g. rcbf_gp_model.flags, which carries RCBF_GP_RT_UPPER)."""
+    from rcbf_amd import _lib
+    assert [f[0] for f in getattr(_lib, pyname)._fields_] == _header_struct_fields(cname)
+    assert _lib.GP_RT_UPPER == 1
