@@ -419,13 +419,26 @@ def pmc_traffic_file(short, B):
     return None, None
 
 
-def rocprof_kernel_us(short, B, kernels):
+DRIVER_FORM = (20, 5)  # the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
+
+
+def rocprof_form(steps, warmup):
+    """Which committed trace is "the same command": the driver's 20-step form
+    (kernel_stats_driver_form_<workload>_B<B>_<tag>.csv, rocprofv3 of
+    `bench.py --steps 20 --warmup 5`) or the default long form
+    (kernel_stats_<workload>_B<B>_<tag>.csv, `bench.py` with --steps 1000)."""
+    return "driver" if (steps, warmup) == DRIVER_FORM else "default"
+
+
+def rocprof_kernel_us(short, B, kernels, form="default"):
     """Mean duration (us) of one timed step's kernels -- the sum of their
     AverageNs -- from the newest committed rocprofv3 --kernel-trace --stats
-    summary of this workload (profiles/r*/kernel_stats_<short>_B<B>_<tag>.csv);
-    (None, None) if there is none."""
+    summary of this workload in the given command form (rocprof_form);
+    (None, None) if there is none.  The driver form falls back to nothing
+    else: a trace of another command is not evidence for its line."""
     import csv
-    for path in _profiles_newest(f"kernel_stats_{short}_B{B}_*.csv"):
+    pat = f"kernel_stats_driver_form_{short}_B{B}_*.csv" if form == "driver" else f"kernel_stats_{short}_B{B}_*.csv"
+    for path in _profiles_newest(pat):
         try:
             rows = list(csv.DictReader(open(path)))
             tot = 0.0
@@ -576,7 +589,8 @@ def main():
     short = workload_short(args)
     traffic, traffic_src = pmc_traffic_file(short, B)
     kernels = dominant_kernels(args, B)
-    k_us_rp, rp_src = rocprof_kernel_us(short, B, kernels)
+    rp_form = rocprof_form(args.steps, args.warmup)
+    k_us_rp, rp_src = rocprof_kernel_us(short, B, kernels, rp_form)
     span = {}
     if world == 1 and not args.cpu_dry_run and not args.no_span and args.workload == "step":
         span = measure_span(env, layer, ctx, dev, B, bps)
@@ -630,6 +644,10 @@ def main():
                      "kernel_us_rocprof": k_us_rp,
                      "frac_rocprof": round(B * bps / (k_us_rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if k_us_rp else None,
                      "rocprof_source": rp_src,
+                     "rocprof_form": (f"driver: rocprofv3 of bench.py --steps {DRIVER_FORM[0]} --warmup {DRIVER_FORM[1]}"
+                                      if rp_form == "driver" else "default: rocprofv3 of bench.py --steps 1000"),
+                     "rocprof_same_command": bool(rp_src) and (rp_form == "driver") == ((args.steps, args.warmup)
+                                                                                          == DRIVER_FORM),
                      "timing": "achieved = bytes_per_launch / kernel_ms; kernel_ms = HIP events around the timed "
                                "region / steps (includes the graph launch and the inter-kernel gaps); host_submit_ms "
                                "= host time spent in the graph replay calls; kernel_us_rocprof = the AverageNs of "
@@ -637,6 +655,14 @@ def main():
                                "traced run: each dispatch serialised with its own completion signal); frac_rocprof "
                                "= bytes_per_launch / kernel_us_rocprof"},
     }
+    if k_us_rp and k_us_rp * 1e-3 > rec["ms_per_step"]:
+        # flagged, not replaced: a traced dispatch carries the tracer's own per-dispatch cost (+2.2-2.5 us on
+        # torch kernels of the same size, profiles/r04/tracer_control_r04b.txt), so its mean can exceed the
+        # untraced wall time per step
+        rec["roofline"]["rocprof_mean_above_wall_per_step"] = True
+        rec["roofline"]["rocprof_note"] = ("the traced mean exceeds ms_per_step: rocprofv3 --kernel-trace serialises "
+                                           "each dispatch with its own completion signal (tracer control: +2.2-2.5 us "
+                                           "per dispatch); frac_rocprof is a traced figure, frac the untraced one")
     if span:
         rec["roofline"]["span"] = span
     if world > 1:  # the spread of the timed region over ranks (value is set by the slowest)

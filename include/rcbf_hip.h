@@ -185,10 +185,13 @@ int rcbf_obs_safe_action_backward(const rcbf_params* prm, int64_t B, const float
  * (the forward the SAC update differentiates, sac_cbf.py:147-158): u_out
  * exactly as the plain forward, plus jac_out (B, n_u, n_u) f64 =
  * d final / d u_rl on the exact active set, through the normaliser, with the
- * clamp folded in (a saturated action's row is NaN, "no gradient").
- * rcbf_safe_action_apply_jac is then the whole backward: grad_u_rl =
- * grad_u . jac over the non-NaN rows, bit for bit what
- * rcbf_[obs_]safe_action_backward computes, without the second solve. */
+ * clamp folded in (a saturated action's row holds RCBF_JAC_NO_GRAD, a NaN
+ * with its own payload, "no gradient"; any other NaN came from the solve and
+ * propagates).  rcbf_safe_action_apply_jac is then the whole backward:
+ * grad_u_rl = grad_u . jac over the rows not marked RCBF_JAC_NO_GRAD, bit for
+ * bit what rcbf_[obs_]safe_action_backward computes, without the second
+ * solve. */
+#define RCBF_JAC_NO_GRAD 0x7FFCD0C0FFEE0000ULL
 int rcbf_safe_action_jac(const rcbf_params* prm, int64_t B, const float* x, const float* u_rl,
                          const float* mu, const float* sigma, float* u_out, double* jac_out,
                          int32_t* status_out, int32_t* fail_flag, hipStream_t stream);

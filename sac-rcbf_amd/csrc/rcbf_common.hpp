@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "rcbf_device.hpp"
 
 // The fused step solves the raw CBF rows (layer_forward's RAW); 0 restores
@@ -31,9 +33,26 @@ __device__ __forceinline__ int64_t env_index() { return (int64_t)blockIdx.x * BS
 // CUs without a 256-thread workgroup (B < 256 CUs x 256) is cut into smaller
 // workgroups that reach more CUs: 128 threads for B >= 32 768 (256-511
 // workgroups), 64 below (one wave per workgroup).
-constexpr int64_t kNumCU = 256;
+// CUs of the current device (256 on an MI355X), queried once per device
+// ordinal and cached: the thresholds follow the part (or partition mode) the
+// launch actually runs on.
+inline int64_t num_cus() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    int cus = cache[dev].load(std::memory_order_relaxed);
+    if (cus <= 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        cache[dev].store(cus, std::memory_order_relaxed);
+    }
+    return cus;
+}
 #ifndef RCBF_STUDY_BLOCK256  // study build: 256-thread workgroups at every batch (the r03 launch)
-inline int block_for_envs(int64_t B) { return B >= kNumCU * 256 ? 256 : B >= kNumCU * 128 ? 128 : 64; }
+inline int block_for_envs(int64_t B) {
+    const int64_t cus = num_cus();
+    return B >= cus * 256 ? 256 : B >= cus * 128 ? 128 : 64;
+}
 #else
 inline int block_for_envs(int64_t) { return 256; }
 #endif

@@ -198,6 +198,9 @@ __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B,
                                               float* s_rt) {
     constexpr int DP = (D + 3) / 4 * 4;  // LDS row stride (float4 reads)
     constexpr float kL2E = 1.4426950408889634f;
+    // gp_qform_dot_staged accumulates the 4 column tiles of a whole 128-column block (acc[0..3] from one
+    // ds_read_b128 of B values) and does not read `sub`: only CT = 4 is correct on that path
+    static_assert(!kGpDot || CT == 4, "the MFMA-argument path (RCBF_GP_DOT_MFMA) needs CT == 4");
 
     // CT column tiles of 32 per wave: 4 (the whole 128-column block) or 2
     // (half of it, twice the workgroups for small query batches)
@@ -585,10 +588,7 @@ int gp_split(const rcbf_gp_model* m, int64_t B) {
 #ifdef RCBF_STUDY_GP_SPLIT  // study builds only: the split count from the environment
     if (const char* e = getenv("RCBF_GP_SPLIT")) return atoi(e) < 1 ? 1 : atoi(e);
 #endif
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-        cus = 256;
+    const int64_t cus = num_cus();
     const int64_t tiles = ((B + kGpRows - 1) / kGpRows) * (m->C_pad / kGpCols) * m->n_s;
     const int64_t want = 6LL * cus;
     if (tiles >= want / 2) return 1;

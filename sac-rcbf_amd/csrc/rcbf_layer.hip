@@ -396,9 +396,12 @@ __global__ void __launch_bounds__(BS) k_safe_action_bwd(rcbf_params prm, int64_t
 // The forward that also keeps what its backward needs (like qpth's
 // QPFunction keeping zhats): u_out exactly as k_safe_action, plus the
 // Jacobian (B, n_u, n_u) f64 with the clamp folded in (a saturated action's
-// row holds NaN: "no gradient"), so the backward is one small elementwise
-// launch (k_apply_jac) instead of a second solve; it computes what
-// k_safe_action_bwd computes, bit for bit.
+// row holds the marker RCBF_JAC_NO_GRAD, a NaN with its own payload: "no
+// gradient"), so the backward is one small elementwise launch (k_apply_jac)
+// instead of a second solve; it computes what k_safe_action_bwd computes, bit
+// for bit.  Only the marker's exact bit pattern means "no gradient": a NaN
+// that the solve itself produces (a degenerate active set) has another
+// pattern and propagates into the gradient as it does in k_safe_action_bwd.
 template <int SOLVER, int MODE, int K, bool FROM_OBS = false, int BS = kBlock>
 __global__ void __launch_bounds__(BS) k_safe_action_jac(rcbf_params prm, int64_t B, const float* __restrict__ x,
                                                         const float* __restrict__ u, const float* __restrict__ mu,
@@ -421,7 +424,8 @@ __global__ void __launch_bounds__(BS) k_safe_action_jac(rcbf_params prm, int64_t
 #pragma unroll
     for (int a = 0; a < NU; ++a)
 #pragma unroll
-        for (int c = 0; c < NU; ++c) jac[(i * NU + a) * NU + c] = pass[a] ? J[a][c] : __builtin_nan("");
+        for (int c = 0; c < NU; ++c)
+            jac[(i * NU + a) * NU + c] = pass[a] ? J[a][c] : __longlong_as_double((long long)RCBF_JAC_NO_GRAD);
 }
 
 template <int NU, int BS>
@@ -435,7 +439,8 @@ __global__ void __launch_bounds__(BS) k_apply_jac(int64_t B, const double* __res
 #pragma unroll
         for (int a = 0; a < NU; ++a) {
             const double j = jac[(i * NU + a) * NU + c];
-            acc += isnan(j) ? 0.0 : (double)grad_u[i * NU + a] * j;
+            const bool no_grad = (unsigned long long)__double_as_longlong(j) == RCBF_JAC_NO_GRAD;
+            acc += no_grad ? 0.0 : (double)grad_u[i * NU + a] * j;
         }
         grad_u_rl[i * NU + c] = (float)acc;
     }

@@ -57,6 +57,8 @@ _U64 = ctypes.c_uint64
 _PRM = ctypes.POINTER(RcbfParams)
 
 
+# rcbf_safe_action_jac: the f64 bit pattern (as int64) of a saturated row's "no gradient" marker
+JAC_NO_GRAD = 0x7FFCD0C0FFEE0000
 GP_RT_UPPER = 1  # rcbf_gp_model.flags: [R | alpha] upper triangular (exact posterior)
 
 

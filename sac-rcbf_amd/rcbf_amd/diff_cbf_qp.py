@@ -182,8 +182,10 @@ def _divide_rows_in_place(Gs, hs):
             Gs.div_(torch.max(torch.abs(Ghs), dim=2, keepdim=True)[0])
 
 
-# qpth.qp.QPFunction.__init__'s keyword arguments (what cbf_layer's solver_args may carry)
-_QPFUNCTION_ARGS = ("eps", "verbose", "notImprovedLim", "maxIter", "solver", "check_Q_spd")
+# qpth.qp.QPFunction.__init__'s keyword arguments that cbf_layer's solver_args may carry.  `verbose`
+# is one of them, but the reference already passes it (QPFunction(verbose=0, **solver_args),
+# diff_cbf_qp.py:139), so solver_args holding it is a duplicate keyword: TypeError there and here.
+_QPFUNCTION_ARGS = ("eps", "notImprovedLim", "maxIter", "solver", "check_Q_spd")
 
 
 class CBFQPLayer:
@@ -287,7 +289,8 @@ class CBFQPLayer:
         """`solver_args` are qpth QPFunction's keyword arguments, as the
         reference passes them (diff_cbf_qp.py:132-139; solve_qp sends
         check_Q_spd, maxIter, notImprovedLim, eps, :107).  An unknown key
-        raises TypeError, as QPFunction(**solver_args) does.  With the
+        raises TypeError, as QPFunction(**solver_args) does, and so does
+        `verbose` (the reference already passes verbose=0, :139).  With the
         interior-point solver (solver=SOLVER_PDIPM) `maxIter` and `eps` set its
         iteration cap and stopping tolerance (notImprovedLim is the
         reference's 10); the exact solvers return the optimum whatever the
@@ -301,6 +304,8 @@ class CBFQPLayer:
         if not solver_args:
             return self._prm
         for k in solver_args:
+            if k == "verbose":  # QPFunction(verbose=0, **solver_args) (diff_cbf_qp.py:139)
+                raise TypeError("QPFunction() got multiple values for keyword argument 'verbose'")
             if k not in _QPFUNCTION_ARGS:
                 raise TypeError(f"QPFunction.__init__() got an unexpected keyword argument '{k}'")
         if self._prm.solver != _lib.SOLVER_PDIPM or ("maxIter" not in solver_args and "eps" not in solver_args):

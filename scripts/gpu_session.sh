@@ -81,7 +81,7 @@ for step in "$@"; do
         python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
       [ -f "$OUT/profdrv/run_kernel_trace.csv" ] && python scripts/trace_summary.py "$OUT/profdrv/run_kernel_trace.csv" \
         "$(wl_kernel cars)" "$OUT/cars_B65536_driver_form_kernel_trace_summary.json"
-      [ -f "$OUT/profdrv/run_kernel_stats.csv" ] && cp "$OUT/profdrv/run_kernel_stats.csv" "$OUT/kernel_stats_driver_form_cars_$TAG.csv" ;;
+      [ -f "$OUT/profdrv/run_kernel_stats.csv" ] && cp "$OUT/profdrv/run_kernel_stats.csv" "$OUT/kernel_stats_driver_form_cars_B65536_$TAG.csv" ;;
     pmc_*)
       run "pmcf_$wl" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcf_$wl" -o run -- \
         python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 $(wl_args "$wl")

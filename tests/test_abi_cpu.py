@@ -219,3 +219,18 @@ def test_ctypes_mirrors_follow_the_header(cname, pyname):
     from rcbf_amd import _lib
     assert [f[0] for f in getattr(_lib, pyname)._fields_] == _header_struct_fields(cname)
     assert _lib.GP_RT_UPPER == 1
+
+
+def test_header_constants_match_the_python_mirror():
+    """Every #define the Python side mirrors has the header's value (e.g. the
+    Jacobian's "no gradient" marker, RCBF_JAC_NO_GRAD, a NaN payload that
+    rcbf_safe_action_apply_jac tells apart from a NaN of the solve)."""
+    import re
+    from rcbf_amd import _lib
+    src = open(os.path.join(ROOT, "include", "rcbf_hip.h")).read()
+    defs = {k: int(v.rstrip("ULul"), 0) for k, v in re.findall(r"#define\s+(RCBF_\w+)\s+(0x[0-9A-Fa-f]+U?L*|\d+)\b", src)}
+    assert defs["RCBF_GP_RT_UPPER"] == _lib.GP_RT_UPPER
+    assert defs["RCBF_JAC_NO_GRAD"] == _lib.JAC_NO_GRAD
+    import struct
+    v = struct.unpack("<d", struct.pack("<Q", _lib.JAC_NO_GRAD))[0]
+    assert v != v and _lib.JAC_NO_GRAD != 0x7FF8000000000000  # a NaN, not the canonical one

@@ -59,6 +59,25 @@ def test_kernel_names_and_profile_lookup():
     assert bench.rocprof_kernel_us("cars", 65536, ["k_not_a_kernel<0>"]) == (None, None)
 
 
+def test_rocprof_figure_comes_from_the_same_command_form(tmp_path, monkeypatch):
+    """The driver's command (--steps 20 --warmup 5) reads only a trace of that
+    command (kernel_stats_driver_form_*), the default form only the long-form
+    trace; neither borrows the other's file."""
+    assert bench.rocprof_form(20, 5) == "driver" and bench.rocprof_form(1000, 20) == "default"
+    prof = tmp_path / "profiles" / "r09"
+    prof.mkdir(parents=True)
+    head = '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+    k = "k_safe_step<0, 0, 1, false, 256, false>"
+    (prof / "kernel_stats_cars_B65536_r09a.csv").write_text(head + f'"void {k}(x)",10,50000,5000.0,90,1,1,1\n')
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.rocprof_kernel_us("cars", 65536, [k], "default") == (5.0, "profiles/r09/kernel_stats_cars_B65536_r09a.csv")
+    assert bench.rocprof_kernel_us("cars", 65536, [k], "driver") == (None, None)
+    (prof / "kernel_stats_driver_form_cars_B65536_r09b.csv").write_text(head + f'"void {k}(x)",88,500000,5800.0,90,1,1,1\n')
+    assert bench.rocprof_kernel_us("cars", 65536, [k], "driver") == (
+        5.8, "profiles/r09/kernel_stats_driver_form_cars_B65536_r09b.csv")
+    assert bench.rocprof_kernel_us("cars", 65536, [k], "default")[0] == 5.0
+
+
 @pytest.mark.parametrize("cfg", [0, 2, 5])
 def test_dry_run_line_carries_the_contract_fields(cfg):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-dry-run", "--steps", "5",

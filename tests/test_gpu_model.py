@@ -54,6 +54,46 @@ def test_model_step_philox_noise_and_gp_mean():
     assert np.max(np.abs(nobs.cpu().numpy() - on)) <= 1e-12 and np.max(np.abs(r.cpu().numpy() - orr)) <= 1e-12
 
 
+def _assert_standard_normal(st, n):
+    """Moment and tail bounds at about 6 standard errors for n samples."""
+    se = 1.0 / np.sqrt(n)
+    assert abs(st["mean"]) < 6 * se and abs(st["var"] - 1.0) < 6 * np.sqrt(2) * se, st
+    assert abs(st["skew"]) < 6 * np.sqrt(6) * se and abs(st["exkurt"]) < 6 * np.sqrt(24) * se, st
+    p3, p4 = 2.699796e-3, 6.334248e-5  # P(|z| > 3), P(|z| > 4) of N(0, 1)
+    assert abs(st["p3"] - p3) < 6 * np.sqrt(p3 / n) and abs(st["p4"] - p4) < 6 * np.sqrt(p4 / n), st
+    assert st["max"] <= np.sqrt(48 * np.log(2)) + 1e-6, st  # 24-bit uniforms: |z| <= 5.768
+
+
+def test_model_step_draw_moments_tails_and_key():
+    """The in-kernel N(0, 1) draws of rcbf_model_step (fp32 Box-Muller on
+    24-bit Philox uniforms, hardware log2 / cos / sin) against the reference's
+    np.random.normal (generate_rollouts.py:31; fp64, values unpinned): over
+    2^20 rows x 4 counters x 2 recoverable components (8.4 M samples) the mean,
+    variance, skewness, excess kurtosis and the P(|z| > 3), P(|z| > 4) tails
+    sit within 6 standard errors of N(0, 1), and |z| never exceeds the
+    truncation bound sqrt(48 ln 2) = 5.768.  The first 4096
+    rows equal the oracle's restatement of the keyed draw
+    (oracle.model_step_normal) to 2e-5."""
+    from rcbf_amd.generate_rollouts import model_step
+    rng = np.random.default_rng(6)
+    B = 1 << 20
+    x = np.stack([rng.uniform(-3, 3, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi, np.pi, B)], 1)
+    obs = O.uni_obs(x)
+    act = rng.uniform(-1, 1, (B, 2))
+    env = _env("Unicycle")
+    base, *_ = model_step(env, obs, act, z=np.zeros((B, 3)))
+    zs = []
+    for counter in range(4):
+        n1, *_ = model_step(env, obs, act, z=None, seed=11, counter=counter)
+        z = ((n1 - base)[:, :2] / (0.02 * 0.2)).cpu().numpy()  # obs[:, :2] = next x, y = mu + dt sd z
+        zs.append(z)
+        if counter == 1:
+            want = O.model_step_normal(11, np.arange(4096), counter, 3)[:, :2]
+            assert np.max(np.abs(z[:4096] - want)) <= 2e-5
+    zs = np.concatenate(zs)
+    _assert_standard_normal(O.normal_moments(zs), zs.size)
+
+
 def test_replay_memory_ring_and_sample():
     from rcbf_amd.replay_memory import ReplayMemory
     rng = np.random.default_rng(0)

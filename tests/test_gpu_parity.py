@@ -157,6 +157,7 @@ def test_jacobian_forward_equals_resolving_backward(mode, k, from_obs):
     u = dev(rng.uniform(-3, 3, (B, n_u)))  # beyond the box: some actions saturate the clamp
     mu = dev(0.01 * rng.normal(0, 1, (B, env.n_s)))
     sg = dev(0.2 * rng.uniform(0, 1, (B, env.n_s)) + 0.05)
+    sg[5] = float("nan")  # a degenerate lane: the solve's own NaN must reach the gradient on both paths
     g = dev(rng.normal(0, 1, (B, n_u)))
     out_a, out_b = torch.empty_like(u), torch.empty_like(u)
     jac = torch.empty(B, n_u, n_u, dtype=torch.float64, device="cuda")
@@ -169,10 +170,18 @@ def test_jacobian_forward_equals_resolving_backward(mode, k, from_obs):
     assert getattr(lib, pre + "_backward")(prm, B, p(inp), p(u), p(mu), p(sg), p(g), p(ga), s) == 0
     assert lib.rcbf_safe_action_apply_jac(B, n_u, p(jac), p(g), p(gb), s) == 0
     torch.cuda.synchronize()
-    assert torch.equal(out_a, out_b)
-    assert torch.equal(ga, gb)
-    saturated = torch.isnan(jac).any(2).any(1)
+    def same(a, b):  # bit-equal values, NaN where the other has NaN
+        return torch.equal(a.isnan(), b.isnan()) and torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
+    assert same(out_a, out_b)
+    assert same(ga, gb)
+    assert bool(ga[5].isnan().any())  # the degenerate lane's NaN was not read as "no gradient"
+    # a saturated action's row holds the RCBF_JAC_NO_GRAD payload, not a generic NaN
+    bits = jac.view(torch.int64)
+    saturated = (bits == _lib.JAC_NO_GRAD).any(2).any(1)
     assert 0 < int(saturated.sum()) < B  # both kinds of rows occur
+    ok = torch.ones(B, dtype=torch.bool, device="cuda")
+    ok[5] = False
+    assert torch.equal(jac[ok].isnan(), (bits[ok] == _lib.JAC_NO_GRAD))  # no other NaN in a finite lane
 
 
 @pytest.mark.parametrize("mode,k", [("SimulatedCars", 0), ("Unicycle", 3)])

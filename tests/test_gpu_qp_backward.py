@@ -156,11 +156,13 @@ def test_cbf_layer_solver_args_reach_the_interior_point():
     want = O.qp_backward(P, q, G, h, False, np.zeros((B, n), np.float32))["z"]
     ok = _non_degenerate(P, q, G, h, False)
     for args in (None, {"check_Q_spd": False, "maxIter": 100000, "notImprovedLim": 10, "eps": 1e-4},
-                 {"maxIter": 2}, {"eps": 1e-12, "verbose": 0}):
+                 {"maxIter": 2}, {"eps": 1e-12, "notImprovedLim": 3}):
         z = layer.cbf_layer(dev(P), dev(q), dev(G), dev(h), solver_args=args)
         assert rel(z.cpu().numpy()[ok], want[ok]) <= 1e-5, args
     with pytest.raises(TypeError):
         layer.cbf_layer(dev(P), dev(q), dev(G), dev(h), solver_args={"max_iter": 5})
+    with pytest.raises(TypeError):  # QPFunction(verbose=0, **solver_args): a duplicate keyword in the reference
+        layer.cbf_layer(dev(P), dev(q), dev(G), dev(h), solver_args={"eps": 1e-12, "verbose": 0})
 
 
 @pytest.mark.parametrize("fixture,mode", [("cars_layer", "SimulatedCars"), ("unicycle3_layer", "Unicycle"),

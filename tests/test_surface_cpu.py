@@ -94,4 +94,8 @@ def test_cbf_layer_solver_args_follow_qpfunction():
     p = pd._solver_params(ref_args)
     assert p is not pd._prm and (p.max_iter, p.eps) == (100000, 1e-4) and (pd._prm.max_iter, pd._prm.eps) == (0, 0.0)
     assert p.gamma_b == pd._prm.gamma_b and p.solver == _lib.SOLVER_PDIPM
-    assert pd._solver_params({"verbose": 0}) is pd._prm
+    # the reference passes verbose=0 itself (diff_cbf_qp.py:139): a second one is a duplicate keyword
+    with pytest.raises(TypeError, match="multiple values for keyword argument 'verbose'"):
+        pd._solver_params({"verbose": 0})
+    with pytest.raises(TypeError, match="multiple values for keyword argument 'verbose'"):
+        exact.cbf_layer(None, None, None, None, solver_args={"eps": 1e-4, "verbose": 0})
