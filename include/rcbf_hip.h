@@ -240,15 +240,21 @@ typedef struct rcbf_gp_model {
     const float* y_scale;  /* (n_s,): train_y std + 1e-8 (dynamics.py:379-380)      */
 } rcbf_gp_model;
 
-/* Floats of workspace rcbf_gp_predict needs for B queries. */
+/* Floats of workspace rcbf_gp_predict needs for B queries.  Its first words
+ * are the arrival counters of the one-launch GEMV path (B <= 8): a workspace
+ * must be ZERO-FILLED before its first use (e.g. torch.zeros); every call
+ * leaves those words zero again.  One workspace per concurrent call. */
 int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B);
 
 /* DynamicsModel.predict_disturbance(test_x) with fitted GPs (dynamics.py:
  * 342-390, gp_model.py:86-114): x (B, n_s) f32 states -> mean (B, n_s) and
  * std (B, n_s) f32, std = sqrt(latent variance + noise) (the likelihood's
  * predictive variance), both rescaled by y_scale.  Exact GP posterior when
- * r = N (gpytorch's LOVE approximates this variance).  Two launches: the
- * k(x, X) [R | alpha] GEMM on the fp32 MFMA, then a per-row finish. */
+ * r = N; gpytorch's fast_pred_var (LOVE, gp_model.py:97-99) above 800
+ * training points is a rank-100 Lanczos R built by the host.  B <= 8: ONE
+ * launch (a streaming GEMV whose last workgroups finish the posterior); B > 8:
+ * the k(x, X) [R | alpha] GEMM on the fp32 MFMA (split-K + combine when the
+ * grid is small), then a per-row finish. */
 int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out,
                     float* std_out, float* workspace, hipStream_t stream);
 

@@ -383,131 +383,234 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
         gp_qform_body<D, CT, SK, false>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha, s_rt);
 }
 
-// Few queries (B <= 8): the posterior is a GEMV per GP, bound by streaming
-// [R | alpha] (n_s N_pad C_pad fp32, 377 MB at the reference's N = 3000), so
-// it skips the MFMA tiles (127 of 128 query rows would be padding) and
-// streams Rt with one 16-B load per lane per training row.  Workgroup
-// (column chunk of 256, row split of 256, GP i): its 256 threads first build
-// k_i(x_b, x_n) of the split's rows for every query into LDS (the arithmetic
-// of k_gp_qform), then wave w accumulates rows 64w..64w+63, and the 4 waves
-// are summed through LDS.  The raw Q values go to qraw in the split-K layout
-// (row split = split index), combined by k_gp_combine.
-constexpr int kGvRows = 256;  // training rows per workgroup (64 per wave)
-constexpr int kGvCols = 256;  // physical Rt columns per workgroup (4 per lane)
+// Few queries (B <= 8, the per-env-step query of main.py, B = 1): the
+// posterior is a GEMV per GP, bound by streaming [R | alpha] (rank 100:
+// 10 x 3008 x 128 fp32 = 15.4 MB), so it skips the MFMA tiles (127 of 128
+// query rows would be padding).  ONE launch, r05:
+//  * tile = (GP i, 128-column block cb, 32-column quarter qc, 128 training
+//    rows): every row of a tile is one 128-B line; thread t streams rows
+//    (t >> 3) + 32 j, j < 4, float4 t & 7, its 4 loads issued before it builds
+//    the kernel values k_i(x_b, x_n) of the tile's rows in LDS.  The exact
+//    factor (RCBF_GP_RT_UPPER) only has tiles below 128 (cb + 1).  Rank 100:
+//    10 x 4 x 24 = 960 workgroups; exact N = 3000: 12 000.
+//  * the 32 x BQ partial of a tile goes to the workspace; the last tile of
+//    block (i, cb) to finish (a per-block arrival counter) sums the block's
+//    partials in a fixed order (deterministic whichever tile is last), forms
+//    sum_{j < r} Q^2 and the mean column; the last block of GP i to finish (a
+//    per-GP counter) writes mean and std.  No combine or finish launch.
+// The counters live in the first words of the workspace, zero before the
+// first call (the caller zero-fills a new workspace) and reset to zero by the
+// workgroups that consume them.  Release / acquire: every thread fences its
+// partial stores before the workgroup barrier and the arrival atomic; the
+// last workgroup fences again before reading (agent scope: the L2s of the 8
+// XCDs are written back / invalidated by the fences).
+constexpr int kGvRows = 128;  // training rows per tile
+constexpr int kGvCols = 32;   // physical Rt columns per tile (one 128-B line per row)
+constexpr int kGvTiles = kGpCols / kGvCols;  // column quarters per 128-column block
+
+// tiles of one GP, and where column block cb's tiles start
+__host__ __device__ inline int gp_gv_kend(const rcbf_gp_model& m, int cb) {
+    return (m.flags & RCBF_GP_RT_UPPER) ? min(m.N_pad, kGpCols * (cb + 1)) : m.N_pad;
+}
+__host__ __device__ inline int gp_gv_rowtiles(const rcbf_gp_model& m, int cb) {
+    return (gp_gv_kend(m, cb) + kGvRows - 1) / kGvRows;
+}
+inline int gp_gv_tiles(const rcbf_gp_model& m) {
+    int t = 0;
+    for (int cb = 0; cb < m.C_pad / kGpCols; ++cb) t += kGvTiles * gp_gv_rowtiles(m, cb);
+    return t;
+}
+// counter words at the start of the workspace: n_s * n_cb block counters, then n_s GP counters
+inline int64_t gp_counter_words(const rcbf_gp_model& m) {
+    return ((int64_t)m.n_s * (m.C_pad / kGpCols + 1) + 63) / 64 * 64;
+}
+
+struct GpCols {
+    int32_t n;
+    int32_t idx[10];
+};
 
 template <int D, int BQ>
 __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
-                                                 int n_rs, float* __restrict__ qraw, int tri) {
+                                                 int T, unsigned* counters, float* part, float* blk,
+                                                 float* meanraw, float* __restrict__ mean_out,
+                                                 float* __restrict__ std_out, GpCols cols,
+                                                 float* __restrict__ mean_cols, float* __restrict__ std_cols) {
     constexpr float kL2E = 1.4426950408889634f;
+    constexpr int RJ = kGvRows / 32;  // rows per thread
+    __shared__ float s_xs[BQ][D];
     __shared__ float s_k[BQ][kGvRows];
-    __shared__ float4 s_red[3][BQ][64];
+    __shared__ float4 s_red[4][BQ][8];
+    __shared__ float s_bsum[4][BQ];
+    __shared__ int s_last;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int i = blockIdx.z;
-    int cc = blockIdx.x, rs = blockIdx.y;
-    if (tri) {  // exact posterior: only the tiles rs <= cc hold nonzero rows; blockIdx.x enumerates them, cc-major
-        int tt = blockIdx.x;
-        cc = 0;
-        while (tt >= min(n_rs, cc + 1)) tt -= min(n_rs, cc + 1), ++cc;
-        rs = tt;
+    const int i = blockIdx.y;
+    const int n_cb = m.C_pad / kGpCols;
+    // tile -> (cb, rc, qc); tiles are cb-major, then row tile, then quarter
+    int tt = blockIdx.x, cb = 0, base = 0;
+    int nrc = gp_gv_rowtiles(m, 0);
+    while (tt >= kGvTiles * nrc) {
+        tt -= kGvTiles * nrc;
+        base += kGvTiles * nrc;
+        ++cb;
+        nrc = gp_gv_rowtiles(m, cb);
     }
+    const int rc = tt / kGvTiles, qc = tt % kGvTiles;
+    const int n0 = rc * kGvRows;
+    const int nrows = min(kGvRows, gp_gv_kend(m, cb) - n0);  // a multiple of 32
+    const int64_t ldc = m.C_pad;
+
+    // 1. this thread's Rt values first: rows n0 + (t >> 3) + 32 j, columns cb*128 + qc*32 + 4 (t & 7) ..+3
+    const float* Rp = m.Rt + ((int64_t)i * m.N_pad + n0 + (t >> 3)) * ldc + cb * kGpCols + qc * kGvCols + 4 * (t & 7);
+    f32x4 v[RJ];
+#pragma unroll
+    for (int j = 0; j < RJ; ++j)
+        v[j] = (32 * j < nrows) ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(Rp + (int64_t)32 * j * ldc))
+                                : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    // 2. the scaled queries (dynamics.py:376: test_x / train_x_std in fp64, then .float())
     const float sl = m.inv_sl[i];
     const float log2s = __log2f(m.outscale[i]);
-    const int n0 = rs * kGvRows;
-    {
+    if (t < BQ * D) {
+        const int b = t / D, k = t % D;
+        const int64_t row = b < B ? b : B - 1;
+        s_xs[b][k] = (float)((double)xq[row * D + k] / m.x_std[k]) * sl;
+    }
+    __syncthreads();
+    // 3. k_i(x_b, x_n) of the tile's rows (the arithmetic of k_gp_qform's level-0 loop)
+    if (t < nrows) {
         const int n = n0 + t;
-        const bool in = n < m.N_pad;
         float xt[D];
 #pragma unroll
-        for (int k = 0; k < D; ++k) xt[k] = in ? m.xt[((int64_t)i * m.N_pad + n) * D + k] : 0.0f;
-        const float tn = in ? -kL2E * m.tn2[(int64_t)i * m.N_pad + n] : 0.0f;
+        for (int k = 0; k < D; ++k) xt[k] = m.xt[((int64_t)i * m.N_pad + n) * D + k];
+        const float tn = -kL2E * m.tn2[(int64_t)i * m.N_pad + n];
 #pragma unroll
         for (int b = 0; b < BQ; ++b) {
-            const int64_t row = b < B ? b : B - 1;
-            float nrm = 0.0f, xs2[D];
+            float nrm = 0.0f;
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                const float xs = (float)((double)xq[row * D + k] / m.x_std[k]) * sl;
-                nrm = fmaf(xs, xs, nrm);
-                xs2[k] = 2.0f * kL2E * xs;
-            }
+            for (int k = 0; k < D; ++k) nrm = fmaf(s_xs[b][k], s_xs[b][k], nrm);
             float arg = fmaf(-kL2E, nrm, log2s) + tn;
 #pragma unroll
-            for (int k = 0; k < D; ++k) arg = fmaf(xs2[k], xt[k], arg);
-            s_k[b][t] = in ? __builtin_amdgcn_exp2f(fminf(arg, log2s)) : 0.0f;
+            for (int k = 0; k < D; ++k) arg = fmaf(2.0f * kL2E * s_xs[b][k], xt[k], arg);
+            s_k[b][t] = __builtin_amdgcn_exp2f(fminf(arg, log2s));
         }
     }
     __syncthreads();
-    const int64_t ldc = m.C_pad;
-    const int pcol = cc * kGvCols + 4 * lane;  // physical column of this lane's first value
-    const bool colin = pcol < m.C_pad;
+    // 4. this thread's rows into 4 columns x BQ queries
     float4 acc[BQ];
 #pragma unroll
     for (int b = 0; b < BQ; ++b) acc[b] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const int nr = min(64, m.N_pad - (n0 + 64 * w));  // rows of this wave (N_pad is a multiple of 32)
-    if (colin && nr > 0) {
-        const float* R = m.Rt + ((int64_t)i * m.N_pad + n0 + 64 * w) * ldc + pcol;
-        const float* kw = &s_k[0][64 * w];
-        if (nr == 64) {
-#pragma unroll 16
-            for (int r = 0; r < 64; ++r) {
-                const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(R + r * ldc));
 #pragma unroll
-                for (int b = 0; b < BQ; ++b) {
-                    const float kv = kw[b * kGvRows + r];
-                    acc[b].x = fmaf(kv, v.x, acc[b].x);
-                    acc[b].y = fmaf(kv, v.y, acc[b].y);
-                    acc[b].z = fmaf(kv, v.z, acc[b].z);
-                    acc[b].w = fmaf(kv, v.w, acc[b].w);
-                }
-            }
-        } else {
-            for (int r = 0; r < nr; ++r) {
-                const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(R + r * ldc));
+    for (int j = 0; j < RJ; ++j) {
+        if (32 * j < nrows) {
 #pragma unroll
-                for (int b = 0; b < BQ; ++b) {
-                    const float kv = kw[b * kGvRows + r];
-                    acc[b].x = fmaf(kv, v.x, acc[b].x);
-                    acc[b].y = fmaf(kv, v.y, acc[b].y);
-                    acc[b].z = fmaf(kv, v.z, acc[b].z);
-                    acc[b].w = fmaf(kv, v.w, acc[b].w);
-                }
+            for (int b = 0; b < BQ; ++b) {
+                const float kv = s_k[b][(t >> 3) + 32 * j];
+                acc[b].x = fmaf(kv, v[j][0], acc[b].x);
+                acc[b].y = fmaf(kv, v[j][1], acc[b].y);
+                acc[b].z = fmaf(kv, v[j][2], acc[b].z);
+                acc[b].w = fmaf(kv, v[j][3], acc[b].w);
             }
         }
     }
-    if (w > 0) {
+    // 5. sum over the 8 row groups of a wave (lane bits 3..5), then over the 4 waves
 #pragma unroll
-        for (int b = 0; b < BQ; ++b) s_red[w - 1][b][lane] = acc[b];
-    }
-    __syncthreads();
-    if (w == 0 && colin) {
-        // physical column 4 l + c of a 128-column block holds logical column 32 c + l
-        const int blk = pcol / kGpCols, l = (pcol % kGpCols) / 4;
+    for (int msk = 8; msk < 64; msk <<= 1) {
 #pragma unroll
         for (int b = 0; b < BQ; ++b) {
-            if (b >= B) break;
-            float4 a = acc[b];
-#pragma unroll
-            for (int u = 0; u < 3; ++u) {
-                const float4 o = s_red[u][b][lane];
-                a.x += o.x, a.y += o.y, a.z += o.z, a.w += o.w;
-            }
-            float* dst = qraw + (((int64_t)i * n_rs + rs) * B + b) * ldc + blk * kGpCols + l;
-            dst[0] = a.x;
-            dst[32] = a.y;
-            dst[64] = a.z;
-            dst[96] = a.w;
+            acc[b].x += __shfl_xor(acc[b].x, msk, 64);
+            acc[b].y += __shfl_xor(acc[b].y, msk, 64);
+            acc[b].z += __shfl_xor(acc[b].z, msk, 64);
+            acc[b].w += __shfl_xor(acc[b].w, msk, 64);
         }
     }
+    if (lane < 8) {
+#pragma unroll
+        for (int b = 0; b < BQ; ++b) s_red[w][b][lane] = acc[b];
+    }
+    __syncthreads();
+    const int tile = base + tt;
+    if (t < 8 * BQ) {
+        const int b = t >> 3, f = t & 7;
+        float4 a = s_red[0][b][f];
+#pragma unroll
+        for (int u = 1; u < 4; ++u) {
+            const float4 o = s_red[u][b][f];
+            a.x += o.x, a.y += o.y, a.z += o.z, a.w += o.w;
+        }
+        reinterpret_cast<float4*>(part)[(((int64_t)i * T + tile) * BQ + b) * (kGvCols / 4) + f] = a;
+    }
+    // 6. arrival at block (i, cb): the last of its tiles reduces the block
+    __threadfence();
+    __syncthreads();
+    if (t == 0) s_last = atomicAdd(&counters[i * n_cb + cb], 1u) == (unsigned)(kGvTiles * nrc - 1);
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const int r_rank = m.r;
+    // thread t: physical column p = t & 127 of the block, queries b = (t >> 7), (t >> 7) + 2, ...
+    const int p = t & 127;
+    const int lc = cb * kGpCols + 32 * (p & 3) + (p >> 2);  // logical column (4 l + c holds 32 c + l)
+    float vq[(BQ + 1) / 2];
+#pragma unroll
+    for (int h = 0; h < (BQ + 1) / 2; ++h) {
+        const int b = (t >> 7) + 2 * h;
+        float q = 0.0f;
+        if (b < BQ) {
+            const float* pp = part + (((int64_t)i * T + base + (p >> 5)) * BQ + b) * kGvCols + (p & 31);
+            for (int r = 0; r < nrc; ++r) q += pp[(int64_t)r * kGvTiles * BQ * kGvCols];
+            if (lc == r_rank && b < B) meanraw[(int64_t)i * BQ + b] = q;
+        }
+        vq[h] = (lc < r_rank) ? q * q : 0.0f;
+    }
+#pragma unroll
+    for (int h = 0; h < (BQ + 1) / 2; ++h) {
+        float x = vq[h];
+#pragma unroll
+        for (int msk = 1; msk < 64; msk <<= 1) x += __shfl_xor(x, msk, 64);
+        if (lane == 0 && (t >> 7) + 2 * h < BQ) s_bsum[w][h] = x;
+    }
+    __syncthreads();
+    if (t < BQ) {  // query b = t: waves 0, 1 hold even b (slot b / 2), waves 2, 3 odd b
+        const int h = t >> 1, w0 = (t & 1) * 2;
+        blk[((int64_t)i * n_cb + cb) * BQ + t] = s_bsum[w0][h] + s_bsum[w0 + 1][h];
+    }
+    // 7. arrival at GP i: the last of its blocks writes mean and std
+    __threadfence();
+    __syncthreads();
+    if (t == 0) {
+        atomicExch(&counters[i * n_cb + cb], 0u);  // consumed: zero for the next call
+        s_last = atomicAdd(&counters[m.n_s * n_cb + i], 1u) == (unsigned)(n_cb - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (t < B) {
+        const int b = t;
+        float q = 0.0f;
+        for (int c = 0; c < n_cb; ++c) q += blk[((int64_t)i * n_cb + c) * BQ + b];
+        const float lat = fmaxf(m.outscale[i] - q, 0.0f);  // latent posterior variance
+        const float var = lat + m.noise[i];                  // likelihood(model(x)).variance
+        const float mu = meanraw[(int64_t)i * BQ + b] * m.y_scale[i];
+        const float sd = sqrtf(var) * m.y_scale[i];
+        if (mean_out) mean_out[(int64_t)b * m.n_s + i] = mu;
+        if (std_out) std_out[(int64_t)b * m.n_s + i] = sd;
+        for (int c = 0; c < cols.n; ++c) {
+            if (cols.idx[c] == i) {
+                if (mean_cols) mean_cols[(int64_t)c * B + b] = mu;
+                if (std_cols) std_cols[(int64_t)c * B + b] = sd;
+            }
+        }
+    }
+    if (t == 0) atomicExch(&counters[m.n_s * n_cb + i], 0u);
 }
 
-// Split-K combine: one wave per (GP i, column block cb, query b) adds the
-// n_split raw Q rows (fixed order) over the block's 128 columns, then
-// partial = sum_{col < r} Q^2 and meanraw = Q(b, r), as k_gp_qform's own epilogue.
-// tri (the GEMV path on an upper-triangular factor): row split s of column chunk
-// col / 256 was not launched when its rows start at or past 256 (chunk + 1).
+// Split-K combine (the MFMA path, B > 8): one wave per (GP i, column block
+// cb, query b) adds the n_split raw Q rows (fixed order) over the block's 128
+// columns, then partial = sum_{col < r} Q^2 and meanraw = Q(b, r), as
+// k_gp_qform's own epilogue.
 __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, int n_cb, int n_split,
                                                     const float* __restrict__ qraw, float* __restrict__ partial,
-                                                    float* __restrict__ meanraw, int tri) {
+                                                    float* __restrict__ meanraw) {
     const int64_t wv = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wv >= (int64_t)m.n_s * n_cb * B) return;
@@ -520,8 +623,7 @@ __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, 
     for (int h = 0; h < 2; ++h) {
         const int col = cb * kGpCols + 64 * h + lane;  // logical column: k_gp_qform stores Q by logical column
         float q = 0.0f;
-        const int ns = tri ? min(n_split, col / kGvCols + 1) : n_split;
-        for (int s = 0; s < ns; ++s) q += qraw[(((int64_t)i * n_split + s) * B + b) * ldc + col];
+        for (int s = 0; s < n_split; ++s) q += qraw[(((int64_t)i * n_split + s) * B + b) * ldc + col];
         v += (col < m.r) ? q * q : 0.0f;
         if (col == m.r) meanraw[(int64_t)i * B + b] = q;
     }
@@ -530,12 +632,8 @@ __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, 
     if (lane == 0) partial[((int64_t)i * n_cb + cb) * B + b] = v;
 }
 
-// mean/std (B, n_s) row-major like predict_disturbance's (n_test, n_s) output.
-// The output dimensions written in column layout (rcbf_gp_predict_cols).
-struct GpCols {
-    int32_t n;
-    int32_t idx[10];
-};
+// mean/std (B, n_s) row-major like predict_disturbance's (n_test, n_s) output;
+// GpCols: the output dimensions written in column layout (rcbf_gp_predict_cols).
 
 // mean and std of GP i at query b (dynamics.py:371-380 after gpytorch)
 __device__ __forceinline__ void gp_mean_std(const rcbf_gp_model& m, int64_t B, int n_cb, const float* partial,
@@ -584,7 +682,7 @@ __global__ void __launch_bounds__(256) k_gp_finish_cols(rcbf_gp_model m, int64_t
 constexpr int kGvMaxB = 8;  // B <= 8: the streaming GEMV path
 
 int gp_split(const rcbf_gp_model* m, int64_t B) {
-    if (B <= kGvMaxB) return (m->N_pad + kGvRows - 1) / kGvRows;  // GEMV row splits
+    if (B <= kGvMaxB) return 1;  // the GEMV path tiles the rows itself
 #ifdef RCBF_STUDY_GP_SPLIT  // study builds only: the split count from the environment
     if (const char* e = getenv("RCBF_GP_SPLIT")) return atoi(e) < 1 ? 1 : atoi(e);
 #endif
@@ -603,12 +701,14 @@ int gp_split(const rcbf_gp_model* m, int64_t B) {
 extern "C" {
 
 int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B) {
-    if (!m || B < 0) return -1;
+    if (!m || B < 0 || m->C_pad < kGpCols || m->n_s < 1) return -1;
     const int64_t n_cb = m->C_pad / kGpCols;
+    const int64_t cw = gp_counter_words(*m);
+    if (B <= kGvMaxB)  // GEMV: tile partials (32 columns x 8 queries), block sums, mean column
+        return cw + (int64_t)m->n_s * gp_gv_tiles(*m) * kGvMaxB * kGvCols + (int64_t)m->n_s * (n_cb + 1) * kGvMaxB;
     const int sk = gp_split(m, B);
     // partials for up to 2 launches per block, + means, + the split-K raw Q tiles
-    const bool raw = sk > 1 || B <= kGvMaxB;
-    return (int64_t)m->n_s * (2 * n_cb + 1) * B + (raw ? (int64_t)sk * m->n_s * B * m->C_pad : 0);
+    return cw + (int64_t)m->n_s * (2 * n_cb + 1) * B + (sk > 1 ? (int64_t)sk * m->n_s * B * m->C_pad : 0);
 }
 
 int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out, float* std_out,
@@ -637,21 +737,18 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
         !m->outscale || !m->noise || !m->y_scale)
         return RCBF_E_NULL;
     const int n_cb = m->C_pad / kGpCols;
-    // CT = 2 (half-width column tiles, twice the workgroups) measured no faster
-    // at B = 256 (profiles/r01/gp_predict_roofline.jsonl), so every batch uses CT = 4
-    const int n_part = n_cb;
-    float* partial = workspace;
-    float* meanraw = workspace + (int64_t)m->n_s * 2 * n_cb * B;
-    const int sk = gp_split(m, B);
-    float* qraw = meanraw + (int64_t)m->n_s * B;
-    const bool tri = (m->flags & RCBF_GP_RT_UPPER) != 0;
+    // the arrival counters of the GEMV path sit first (zero-filled by the caller once, left zero by every call)
+    unsigned* counters = reinterpret_cast<unsigned*>(workspace);
+    float* ws = workspace + gp_counter_words(*m);
     if (B <= kGvMaxB) {
-        const int n_cc = (m->C_pad + kGvCols - 1) / kGvCols;
-        int tiles = 0;  // upper-triangular factor: only the tiles rs <= cc (k_gp_gemv decodes them)
-        for (int c = 0; c < n_cc; ++c) tiles += sk < c + 1 ? sk : c + 1;
-        dim3 gv(tri ? (unsigned)tiles : (unsigned)n_cc, tri ? 1u : (unsigned)sk, (unsigned)m->n_s);
-#define RCBF_GV_L(DD, BB) \
-    hipLaunchKernelGGL((k_gp_gemv<DD, BB>), gv, dim3(256), 0, stream, *m, B, x, sk, qraw, (int)tri)
+        const int T = gp_gv_tiles(*m);
+        float* part = ws;
+        float* blk = part + (int64_t)m->n_s * T * kGvMaxB * kGvCols;
+        float* mraw = blk + (int64_t)m->n_s * n_cb * kGvMaxB;
+        dim3 gv((unsigned)T, (unsigned)m->n_s);
+#define RCBF_GV_L(DD, BB)                                                                                  \
+    hipLaunchKernelGGL((k_gp_gemv<DD, BB>), gv, dim3(256), 0, stream, *m, B, x, T, counters, part, blk, mraw, \
+                       mean_out, std_out, gc, mean_cols, std_cols)
 #define RCBF_GV_B(DD)           \
     do {                        \
         if (B == 1)             \
@@ -675,7 +772,16 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
         }
 #undef RCBF_GV_B
 #undef RCBF_GV_L
-    } else {
+        return launch_status();
+    }
+    // CT = 2 (half-width column tiles, twice the workgroups) measured no faster
+    // at B = 256 (profiles/r01/gp_predict_roofline.jsonl), so every batch uses CT = 4
+    const int n_part = n_cb;
+    float* partial = ws;
+    float* meanraw = ws + (int64_t)m->n_s * 2 * n_cb * B;
+    const int sk = gp_split(m, B);
+    float* qraw = meanraw + (int64_t)m->n_s * B;
+    {
         dim3 g((unsigned)((B + kGpRows - 1) / kGpRows), (unsigned)n_part, (unsigned)(m->n_s * sk));
 #define RCBF_GP_L(DD)                                                                                           \
     do {                                                                                                        \
@@ -698,10 +804,10 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
         }
 #undef RCBF_GP_L
     }
-    if (sk > 1 || B <= kGvMaxB) {
+    if (sk > 1) {
         const int64_t waves = (int64_t)m->n_s * n_cb * B;
         hipLaunchKernelGGL(k_gp_combine, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, *m, B, n_cb, sk,
-                           qraw, partial, meanraw, (int)(tri && B <= kGvMaxB));
+                           qraw, partial, meanraw);
     }
     if (mean_out || std_out) {
         const int64_t tot = B * m->n_s;

@@ -37,7 +37,13 @@ class DynamicsModel:
         self.history_counter = 0
         self.train_x = None
         self.train_y = None
-        self.gp_rank = getattr(args, "gp_rank", None)  # None: exact posterior variance
+        # the GP variance factor: "love" (default) follows the reference's gpytorch.settings.fast_pred_var()
+        # (gp_model.py:97-99): exact (Cholesky) up to 800 training points, a Lanczos root of rank <= 100 above;
+        # "exact" always takes the exact posterior.  args.gp_rank (an int) forces a Lanczos size.
+        self.gp_variance = getattr(args, "gp_variance", "love")
+        if self.gp_variance not in ("love", "exact"):
+            raise ValueError(f"gp_variance must be 'love' or 'exact', got {self.gp_variance!r}")
+        self.gp_rank = getattr(args, "gp_rank", None)
         if hasattr(args, "l_p"):
             self.l_p = args.l_p
         self.device = torch.device("cuda" if getattr(args, "cuda", False) else "cpu")
@@ -81,9 +87,17 @@ class DynamicsModel:
             train_x = self.disturbance_history["state"]
             train_y = self.disturbance_history["disturbance"]
         self.disturb_estimators = gp.fit(train_x, train_y, MAX_STD[self.env.dynamics_mode], training_iter,
-                                         rank=self.gp_rank)
+                                         rank=self._gp_factor_rank(len(train_x)))
         self.train_x = np.array(train_x, copy=True)
         self.train_y = np.array(train_y, copy=True)
+
+    def _gp_factor_rank(self, N):
+        """Lanczos size of the variance factor for N training points (None:
+        the exact Cholesky inverse root)."""
+        if self.gp_rank is not None:
+            return int(self.gp_rank)
+        from . import gp
+        return gp.love_rank(N) if self.gp_variance == "love" else None
 
     # -- GP persistence and seeding (dynamics.py:392-425; main.py:136,183,313) --
     def save_disturbance_models(self, output):
@@ -100,6 +114,8 @@ class DynamicsModel:
         torch.save(weights, f"{output}/gp_models.pkl")
         torch.save(torch.as_tensor(self.train_x), f"{output}/gp_models_train_x.pkl")
         torch.save(torch.as_tensor(self.train_y), f"{output}/gp_models_train_y.pkl")
+        if self.disturb_estimators.love_init is not None:  # the Lanczos start vectors: a reload rebuilds the same root
+            torch.save(self.disturb_estimators.love_init, f"{output}/gp_models_love_init.pkl")
 
     def load_disturbance_models(self, output):
         """Restores what save_disturbance_models wrote (None -> no-op); any
@@ -116,7 +132,11 @@ class DynamicsModel:
             hyper = [(float(w["lengthscale"]), float(w["outputscale"]), float(w["noise"])) for w in weights]
             if len(hyper) != self.n_s:
                 raise ValueError("state dimension mismatch")
-            self.disturb_estimators = gp.GPDisturbanceModel(tx, ty, hyper, rank=self.gp_rank)
+            import os
+            init_path = f"{output}/gp_models_love_init.pkl"
+            init = torch.load(init_path, weights_only=True) if os.path.exists(init_path) else None
+            self.disturb_estimators = gp.GPDisturbanceModel(tx, ty, hyper, rank=self._gp_factor_rank(len(tx)),
+                                                            love_init=init)
             self.train_x, self.train_y = tx, ty
         except Exception:
             raise Exception("Could not load GP models from {}".format(output))

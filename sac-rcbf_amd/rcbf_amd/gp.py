@@ -11,10 +11,22 @@ DynamicsModel.fit_gp_model / predict_disturbance (rcbf_sac/dynamics.py:296-390).
   55-78).  gpytorch itself is not installed here, so this is a restatement of
   its published algorithm (fp64 on the device instead of its fp32), parity
   unpinned against gpytorch; tests pin it to the numpy oracle.
-* Predict (the per-step hot path): rcbf_gp_predict, the exact GP posterior
-  mean and predictive std on the fp32 MFMA (csrc/rcbf_gp.hip).  gpytorch's
-  fast_pred_var (LOVE, gp_model.py:97) approximates this variance; `rank` < N
-  gives the analogous low-rank variance (top-r eigenpairs of K + nI).
+* Predict (the per-step hot path): rcbf_gp_predict, the GP posterior mean
+  and predictive std on the device (csrc/rcbf_gp.hip) from [R | alpha],
+  where R R^T ~ (K + nI)^-1.  The reference predicts under
+  gpytorch.settings.fast_pred_var() (LOVE, gp_model.py:97-99): gpytorch's
+  root_inv_decomposition takes the Cholesky inverse root L^-T (the exact
+  posterior) up to max_cholesky_size = 800 training points and, above that,
+  a Lanczos inverse root of rank <= max_root_decomposition_size = 100 from one
+  random start vector (torch.randn).  love_rank(N) restates that choice and
+  love_inv_root restates the Lanczos root (linear_operator's lanczos_tridiag
+  with full reorthogonalisation, then the Ritz decomposition), in fp64 on the
+  device; the oracle restates it again in numpy (oracle.love_inv_root).  The
+  start vectors are drawn from torch's global CPU generator and kept
+  (`love_init`), so a fit is reproducible under torch.manual_seed.  Parity
+  against gpytorch itself is unpinned (not installed; its start vector is
+  random anyway).  The mean uses the exact solve, the converged value of
+  gpytorch's preconditioned CG.
 """
 import ctypes
 import math
@@ -26,6 +38,79 @@ from . import _lib
 
 _PAD_N = 32
 _PAD_C = 128
+
+
+MAX_CHOLESKY_SIZE = 800  # gpytorch.settings.max_cholesky_size default
+MAX_ROOT_SIZE = 100      # gpytorch.settings.max_root_decomposition_size default
+
+
+def love_rank(N):
+    """The variance factor gpytorch's fast_pred_var builds for N training
+    points: None = the Cholesky inverse root (exact) at N <= 800, else a
+    Lanczos inverse root of size min(100, N)."""
+    return None if N <= MAX_CHOLESKY_SIZE else min(MAX_ROOT_SIZE, N)
+
+
+def lanczos_tridiag(C, init_vec, max_iter, tol=1e-5):
+    """linear_operator.utils.lanczos.lanczos_tridiag for one SPD matrix C
+    (N, N) and one start vector (N,) (torch, C's device and dtype): Lanczos
+    with classical Gram-Schmidt reorthogonalisation against all earlier
+    vectors, up to 10 extra passes while an inner product exceeds tol; stops
+    when beta <= 1e-6 or the extra passes fail.  Returns Q (N, k), T (k, k)."""
+    N = C.shape[0]
+    num_iter = min(int(max_iter), N)
+    Q = torch.zeros(num_iter, N, dtype=C.dtype, device=C.device)
+    T = torch.zeros(num_iter, num_iter, dtype=C.dtype, device=C.device)
+    v = init_vec.to(dtype=C.dtype, device=C.device)
+    q0 = v / torch.linalg.vector_norm(v)
+    Q[0] = q0
+    r = C @ q0
+    a0 = q0 @ r
+    r = r - a0 * q0
+    b0 = torch.linalg.vector_norm(r)
+    T[0, 0] = a0
+    if num_iter > 1:
+        T[0, 1] = b0
+        T[1, 0] = b0
+        Q[1] = r / b0
+    k = 0
+    for k in range(1, num_iter):
+        r = C @ Q[k] - Q[k - 1] * T[k, k - 1]
+        ac = Q[k] @ r
+        T[k, k] = ac
+        if k + 1 < num_iter:
+            r = r - ac * Q[k]
+            Qk = Q[:k + 1]
+            r = r - Qk.t() @ (Qk @ r)
+            bc = torch.linalg.vector_norm(r)
+            r = r / bc
+            T[k, k + 1] = bc
+            T[k + 1, k] = bc
+            could = False
+            for _ in range(10):
+                if not bool(((Qk @ r) > tol).any()):
+                    could = True
+                    break
+                r = r - Qk.t() @ (Qk @ r)
+                r = r / torch.linalg.vector_norm(r)
+            Q[k + 1] = r
+            if float(bc.abs()) <= 1e-6 or not could:
+                break
+    n = k + 1
+    return Q[:n].t(), T[:n, :n]
+
+
+def love_inv_root(C, init_vec, max_iter):
+    """LOVE's inverse root (linear_operator RootDecomposition with
+    inverse=True): R = Q V diag(lam)^-1/2 from the Lanczos T = V diag(lam)
+    V^T, negative Ritz values masked (their columns zero), so
+    R R^T = Q T^-1 Q^T ~ C^-1.  Returns R (N, k)."""
+    Q, T = lanczos_tridiag(C, init_vec, max_iter)
+    lam, V = torch.linalg.eigh(T)
+    keep = lam >= 0
+    V = V * keep[None, :].to(V.dtype)
+    lam = torch.where(keep, lam, torch.ones_like(lam))
+    return (Q @ V) / torch.sqrt(lam)[None, :]
 
 
 def _softplus(x):
@@ -72,15 +157,23 @@ class GPDisturbanceModel:
     """The n_s fitted GPs of a DynamicsModel, resident on the device in the
     layout rcbf_gp_predict reads (include/rcbf_hip.h rcbf_gp_model)."""
 
-    def __init__(self, train_x, train_y, hyper, device=None, rank=None):
+    def __init__(self, train_x, train_y, hyper, device=None, rank=None, love_init=None):
         """train_x, train_y: (N, n_s) raw history (dynamics.py:307-312);
-        hyper: per dim (lengthscale, outputscale, noise)."""
+        hyper: per dim (lengthscale, outputscale, noise).  rank None: the
+        exact posterior (Cholesky inverse root); rank r: LOVE's Lanczos
+        inverse root of size <= r (love_rank(N) gives gpytorch's choice) from
+        the start vectors love_init (n_s, N) (default: torch.randn from the
+        global CPU generator, as gpytorch draws its own)."""
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         tx = np.asarray(train_x, np.float64)
         ty = np.asarray(train_y, np.float64)
         N, n_s = tx.shape
         self.n_s, self.N, self.device = n_s, N, dev
-        self.r = N if rank is None else int(min(rank, N))
+        self.rank = None if rank is None else int(rank)
+        self.love_init = None
+        if self.rank is not None:
+            self.love_init = (torch.randn(n_s, N, dtype=torch.float64) if love_init is None else
+                              torch.as_tensor(np.asarray(love_init, np.float64)).reshape(n_s, N).clone())
         x_std = tx.std(axis=0)
         y_std = ty.std(axis=0)
         # dynamics.py:315-318: training data normalised by std + 1e-8, as fp32 tensors
@@ -88,28 +181,30 @@ class GPDisturbanceModel:
         yn = torch.as_tensor(ty / (y_std + 1e-8), dtype=torch.float32, device=dev)
         self.hyper = [tuple(map(float, h)) for h in hyper]
         N_pad = -(-N // _PAD_N) * _PAD_N
-        C_pad = -(-(self.r + 1) // _PAD_C) * _PAD_C
-        xt = torch.zeros(n_s, N_pad, n_s, dtype=torch.float32, device=dev)
-        Rt = torch.zeros(n_s, N_pad, C_pad, dtype=torch.float32, device=dev)
         x64 = xn.double()
         d2 = torch.cdist(x64, x64).pow(2)
         eye = torch.eye(N, dtype=torch.float64, device=dev)
+        Rs, alphas = [], []
         for i, (ls, os_, nz) in enumerate(self.hyper):
-            isl = 1.0 / (math.sqrt(2.0) * ls)
-            xt[i, :N] = (xn * np.float32(isl))
             C = os_ * torch.exp(-0.5 * d2 / (ls * ls)) + nz * eye
             y = yn[:, i].double()
-            if self.r == N:  # exact: C^-1 = L^-T L^-1, R = L^-T
-                L = torch.linalg.cholesky(C)
-                Linv = torch.linalg.solve_triangular(L, eye, upper=False)
-                R = Linv.t()
-                alpha = torch.cholesky_solve(y[:, None], L)[:, 0]
-            else:            # top-r eigenpairs of C (the subspace LOVE's Lanczos captures)
-                lam, U = torch.linalg.eigh(C)
-                R = U[:, -self.r:] / torch.sqrt(lam[-self.r:])[None]
-                alpha = torch.linalg.solve(C, y)
-            Rt[i, :N, :self.r] = R.float()
-            Rt[i, :N, self.r] = alpha.float()
+            L = torch.linalg.cholesky(C)
+            alpha = torch.cholesky_solve(y[:, None], L)[:, 0]
+            if self.rank is None:  # exact: C^-1 = L^-T L^-1, R = L^-T
+                R = torch.linalg.solve_triangular(L, eye, upper=False).t()
+            else:                  # LOVE: Lanczos inverse root of size <= rank (gp_model.py:97-99)
+                R = love_inv_root(C, self.love_init[i], self.rank)
+            Rs.append(R)
+            alphas.append(alpha)
+        # one factor width for all GPs (a Lanczos run may stop early): zero columns add nothing to |k R|^2
+        self.r = max(R.shape[1] for R in Rs)
+        C_pad = -(-(self.r + 1) // _PAD_C) * _PAD_C
+        xt = torch.zeros(n_s, N_pad, n_s, dtype=torch.float32, device=dev)
+        Rt = torch.zeros(n_s, N_pad, C_pad, dtype=torch.float32, device=dev)
+        for i, (ls, os_, nz) in enumerate(self.hyper):
+            xt[i, :N] = (xn * np.float32(1.0 / (math.sqrt(2.0) * ls)))
+            Rt[i, :N, :Rs[i].shape[1]] = Rs[i].float()
+            Rt[i, :N, self.r] = alphas[i].float()
         self.xt = xt.contiguous()
         self.tn2 = (xt.double() ** 2).sum(-1).float().contiguous()
         # lane-interleave each 128-column block: physical 4 l + c <- logical 32 c + l
@@ -121,7 +216,7 @@ class GPDisturbanceModel:
         self.noise = torch.tensor([h[2] for h in self.hyper], dtype=torch.float32, device=dev)
         self.y_scale = torch.as_tensor(y_std + 1e-8, dtype=torch.float32, device=dev)
         # exact: R = L^-T is upper triangular, so the kernels skip the zero rows of each column block
-        flags = _lib.GP_RT_UPPER if self.r == N else 0
+        flags = _lib.GP_RT_UPPER if self.rank is None else 0
         self._m = _lib.RcbfGpModel(n_s, N, N_pad, self.r, C_pad, flags, *(t.data_ptr() for t in (
             self.xt, self.tn2, self.Rt, self.x_std, self.inv_sl, self.outscale, self.noise, self.y_scale)))
         self._ws = torch.empty(0, dtype=torch.float32, device=dev)
@@ -140,7 +235,7 @@ class GPDisturbanceModel:
         std = torch.empty_like(mean)
         need = int(lib.rcbf_gp_workspace_floats(ctypes.byref(self._m), B))
         if self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
+            self._ws = torch.zeros(need, dtype=torch.float32, device=self.device)  # counters start at zero
         rc = lib.rcbf_gp_predict(ctypes.byref(self._m), B, _lib.ptr(x), _lib.ptr(mean), _lib.ptr(std),
                                  _lib.ptr(self._ws), _lib.stream_of(self.device))
         _lib.check(rc, "rcbf_gp_predict")
@@ -163,7 +258,7 @@ class GPDisturbanceModel:
         sr = torch.empty_like(mr) if rows else None
         need = int(lib.rcbf_gp_workspace_floats(ctypes.byref(self._m), B))
         if self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
+            self._ws = torch.zeros(need, dtype=torch.float32, device=self.device)  # counters start at zero
         rc = lib.rcbf_gp_predict_cols(ctypes.byref(self._m), B, _lib.ptr(x), _lib.ptr(mr), _lib.ptr(sr), carr,
                                       len(cols), _lib.ptr(mc), _lib.ptr(sc), _lib.ptr(self._ws),
                                       _lib.stream_of(self.device))
@@ -182,12 +277,13 @@ class GPDisturbanceModel:
         return 2 * self.N * self._m.C_pad * self.n_s
 
 
-def fit(train_x, train_y, prior_std, training_iter=70, device=None, rank=None):
-    """DynamicsModel.fit_gp_model (dynamics.py:296-340) -> GPDisturbanceModel."""
+def fit(train_x, train_y, prior_std, training_iter=70, device=None, rank=None, love_init=None):
+    """DynamicsModel.fit_gp_model (dynamics.py:296-340) -> GPDisturbanceModel
+    (rank: see GPDisturbanceModel; DynamicsModel passes love_rank(N))."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     tx = np.asarray(train_x, np.float64)
     ty = np.asarray(train_y, np.float64)
     xn = torch.as_tensor(tx / (tx.std(axis=0) + 1e-8), dtype=torch.float32, device=dev).double()
     yn = torch.as_tensor(ty / (ty.std(axis=0) + 1e-8), dtype=torch.float32, device=dev).double()
     hyper = [train_hyperparameters(xn, yn[:, i], float(prior_std[i]), training_iter) for i in range(tx.shape[1])]
-    return GPDisturbanceModel(tx, ty, hyper, device=dev, rank=rank)
+    return GPDisturbanceModel(tx, ty, hyper, device=dev, rank=rank, love_init=love_init)

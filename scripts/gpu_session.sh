@@ -107,6 +107,11 @@ for step in "$@"; do
         env $lib timeout -k 10 200 python scripts/gp_bench.py 10 3000 > "$OUT/gp_${n}_$r.log" 2>&1 || exit 1
         echo "$n $(tail -1 "$OUT/gp_${n}_$r.log")" >> "$OUT/gpab_sum.txt"
       done; done ;;
+    gpt)    run gpt 600 python -u -m pytest tests/test_gpu_gp.py tests/test_gpu_parity.py -q -rf --timeout 300 --timeout-method thread ;;
+    gpgb)   run gpgb 300 python -u scripts/gp_graph_bench.py ;;
+    profgp) run profgp 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profgp" -o run -- \
+              python3 scripts/gp_graph_bench.py 20 5
+      [ -f "$OUT/profgp/run_kernel_stats.csv" ] && cp "$OUT/profgp/run_kernel_stats.csv" "$OUT/kernel_stats_gp_graph_bench_$TAG.csv" ;;
     abjac) bash scripts/ab_multi.sh "$TAG/abjac" "jacgi" c5 || exit 1 ;;
     abbs)  bash scripts/ab_multi.sh "$TAG/abbs" "bs256" c2 c3 c4s c5 || exit 1 ;;
     absin) bash scripts/ab_multi.sh "$TAG/absin" "nosincos" u5 u3 || exit 1 ;;

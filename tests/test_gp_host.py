@@ -57,9 +57,107 @@ def test_device_layout_reproduces_exact_posterior(n_s, N, rank):
         lat = np.maximum(float(m.outscale[i]) - (Q[:, :m.r] ** 2).sum(1), 0.0)
         mean[:, i] = Q[:, m.r] * float(m.y_scale[i])
         std[:, i] = np.sqrt(lat + float(m.noise[i])) * float(m.y_scale[i])
-    mo, so = O.gp_predict(q, tx, ty, hyper, rank=rank)
+    mo, so = O.gp_predict(q, tx, ty, hyper, rank=rank, love_init=None if rank is None else m.love_init.numpy())
     assert np.max(np.abs(mean - mo)) <= 1e-5 * np.max(np.abs(mo)) + 1e-7
     assert np.max(np.abs(std - so) / so) <= 1e-5
+
+
+def _kernel_matrix(rng, N, D, ls=1.4, os_=0.3, nz=0.04):
+    x = rng.normal(0, 1, (N, D))
+    d2 = ((x[:, None] - x[None]) ** 2).sum(-1)
+    return os_ * np.exp(-0.5 * d2 / ls ** 2) + nz * np.eye(N)
+
+
+def test_love_rank_follows_gpytorch_settings():
+    """fast_pred_var's root_inv_decomposition: Cholesky (exact) up to
+    max_cholesky_size = 800 points, a Lanczos root of max_root_decomposition_size
+    = 100 above (gp_model.py:97-99); host and oracle agree."""
+    from rcbf_amd import gp
+    for N, want in ((10, None), (800, None), (801, 100), (3000, 100)):
+        assert gp.love_rank(N) == want == O.love_rank(N)
+
+
+def test_lanczos_restatement_is_a_lanczos_decomposition():
+    """oracle.lanczos_tridiag: Q orthonormal, Q^T C Q = T tridiagonal, and the
+    first column is the normalised start vector (N = 900, 100 steps)."""
+    rng = np.random.default_rng(2)
+    C = _kernel_matrix(rng, 900, 10)
+    v = rng.normal(0, 1, 900)
+    Q, T = O.lanczos_tridiag(C, v, 100)
+    assert Q.shape == (900, 100) and T.shape == (100, 100)
+    assert np.max(np.abs(Q.T @ Q - np.eye(100))) <= 1e-12
+    assert np.max(np.abs(Q.T @ C @ Q - T)) <= 1e-12 * np.abs(T).max()
+    assert np.array_equal(T, np.triu(np.tril(T, 1), -1)) and np.allclose(Q[:, 0], v / np.linalg.norm(v))
+
+
+def test_host_lanczos_root_matches_the_oracle():
+    """rcbf_amd.gp.love_inv_root (torch, what the fit runs on the device) and
+    oracle.love_inv_root (numpy) on the same matrix and start vector: the same
+    Lanczos root, R R^T within 1e-10 of its scale."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(3)
+    C = _kernel_matrix(rng, 1000, 10)
+    v = rng.normal(0, 1, 1000)
+    Rh = gp.love_inv_root(torch.as_tensor(C), torch.as_tensor(v), 100).numpy()
+    Ro = O.love_inv_root(C, v, 100)
+    assert Rh.shape == Ro.shape == (1000, 100)
+    assert np.max(np.abs(Rh @ Rh.T - Ro @ Ro.T)) <= 1e-10 * np.abs(Ro @ Ro.T).max()
+
+
+def test_love_variance_bounds_the_exact_variance():
+    """LOVE's R R^T = Q T^-1 Q^T <= C^-1 (Loewner order), so its predictive
+    std is never below the exact posterior's, and a Lanczos root of full size
+    (Krylov space = the whole space) reproduces the exact posterior.  The mean
+    is the exact solve in both."""
+    rng = np.random.default_rng(4)
+    N, D = 1200, 10
+    tx = rng.normal(0, 1, (N, D))
+    ty = 0.1 * np.sin(tx @ rng.normal(0, 1, (D, D))) + rng.normal(0, 0.05, (N, D))
+    hyper = [(1.5, 0.2, 0.05)] * D
+    init = rng.normal(0, 1, (D, N))
+    q = rng.normal(0, 1, (64, D)) * tx.std(0)
+    me, se = O.gp_predict(q, tx, ty, hyper)
+    ml, sl = O.gp_predict(q, tx, ty, hyper, rank=100, love_init=init)
+    assert np.array_equal(me, ml)
+    assert np.all(sl >= se * (1 - 1e-12)) and np.max(sl / se) > 1.001  # a real (one-sided) approximation
+    n = 200
+    mf, sf = O.gp_predict(q, tx[:n], ty[:n], hyper)
+    mr, sr = O.gp_predict(q, tx[:n], ty[:n], hyper, rank=n, love_init=init[:, :n])
+    assert np.max(np.abs(sr / sf - 1)) <= 1e-9
+
+
+def test_dynamics_model_variance_setting():
+    """DynamicsModel picks the variance factor as the reference's gpytorch
+    does: exact up to 800 points, Lanczos 100 above; gp_variance='exact'
+    always exact; gp_rank forces a size."""
+    from rcbf_amd.dynamics import DynamicsModel
+    env = types.SimpleNamespace(dynamics_mode="Unicycle", dt=0.02)
+    dm = DynamicsModel(env, types.SimpleNamespace(cuda=False))
+    assert dm.gp_variance == "love" and dm._gp_factor_rank(800) is None and dm._gp_factor_rank(3000) == 100
+    dx = DynamicsModel(env, types.SimpleNamespace(cuda=False, gp_variance="exact"))
+    assert dx._gp_factor_rank(3000) is None
+    dr = DynamicsModel(env, types.SimpleNamespace(cuda=False, gp_rank=64))
+    assert dr._gp_factor_rank(3000) == 64 and dr._gp_factor_rank(100) == 64
+    with pytest.raises(ValueError):
+        DynamicsModel(env, types.SimpleNamespace(cuda=False, gp_variance="svd"))
+
+
+def test_love_model_is_reproducible_from_its_start_vectors():
+    """GPDisturbanceModel(rank=r) draws its Lanczos start vectors from torch's
+    global CPU generator (as gpytorch draws torch.randn), keeps them, and the
+    same vectors rebuild the same factor bit for bit."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(5)
+    tx = rng.normal(0, 1, (300, 3))
+    ty = rng.normal(0, 0.1, (300, 3))
+    hyper = [(1.2, 0.3, 0.05)] * 3
+    torch.manual_seed(7)
+    a = gp.GPDisturbanceModel(tx, ty, hyper, device="cpu", rank=40)
+    torch.manual_seed(7)
+    b = gp.GPDisturbanceModel(tx, ty, hyper, device="cpu", rank=40)
+    c = gp.GPDisturbanceModel(tx, ty, hyper, device="cpu", rank=40, love_init=a.love_init)
+    assert a.love_init.shape == (3, 300) and torch.equal(a.love_init, b.love_init)
+    assert torch.equal(a.Rt, b.Rt) and torch.equal(a.Rt, c.Rt) and a.r == 40 and a._m.flags == 0
 
 
 def _dyn(mode):

@@ -42,6 +42,8 @@ def test_gp_predict_vs_oracle(n_s, N, B):
 
 
 def test_gp_predict_low_rank():
+    """A Lanczos inverse root of size 64 (LOVE's algorithm, forced size) vs
+    the oracle's restatement on the same start vectors."""
     from rcbf_amd import gp
     rng = np.random.default_rng(5)
     tx, ty = _data(rng, 500, 3)
@@ -49,7 +51,55 @@ def test_gp_predict_low_rank():
     model = gp.GPDisturbanceModel(tx, ty, hyper, rank=64)
     q = (rng.normal(0, 1, (1000, 3)) * tx.std(0)).astype(np.float32)
     mean, std = model.predict(torch.as_tensor(q, device="cuda"))
-    mo, so = O.gp_predict(q, tx, ty, hyper, rank=64)
+    mo, so = O.gp_predict(q, tx, ty, hyper, rank=64, love_init=model.love_init.numpy())
+    _check(mean.cpu().numpy(), std.cpu().numpy(), mo, so)
+
+
+def test_gp_predict_love_default_vs_oracle():
+    """The reference's own prediction algorithm at its gp_model_size (3000,
+    main.py:247): gpytorch's fast_pred_var takes a rank-100 Lanczos inverse
+    root above 800 points (gp_model.py:97-99, restated in oracle.love_inv_root;
+    parity vs gpytorch unpinned).  The device factor from the same start
+    vectors, through every path (GEMV B <= 8, split-K, single pass), meets
+    the oracle at the same bars as the exact posterior; and LOVE's std is the
+    one-sided approximation (never below exact, by more than the fp32 bar)."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(31)
+    tx, ty = _data(rng, 3000, 10)
+    hyper = [(rng.uniform(0.8, 2.5), rng.uniform(0.05, 0.5), rng.uniform(0.01, 0.2)) for _ in range(10)]
+    assert gp.love_rank(3000) == 100
+    model = gp.GPDisturbanceModel(tx, ty, hyper, rank=gp.love_rank(3000))
+    assert model.r == 100 and model._m.C_pad == 128
+    sizes = [1, 3, 8, 256, 1000]
+    q = (rng.normal(0, 1, (sum(sizes), 10)) * tx.std(0)).astype(np.float32)
+    mo, so = O.gp_predict(q, tx, ty, hyper, rank=100, love_init=model.love_init.numpy())
+    _, se = O.gp_predict(q, tx, ty, hyper)
+    b0 = 0
+    for B in sizes:
+        sl = slice(b0, b0 + B)
+        mean, std = model.predict(torch.as_tensor(q[sl], device="cuda"))
+        _check(mean.cpu().numpy(), std.cpu().numpy(), mo[sl], so[sl])
+        assert np.all(std.cpu().numpy() >= se[sl] * (1 - 1e-4)), B
+        b0 += B
+
+
+def test_dynamics_model_love_fit_and_predict():
+    """DynamicsModel's default variance setting above 800 points: the fit
+    builds LOVE's rank-100 factor and predict_disturbance runs it on the
+    device (vs the oracle on the model's own start vectors)."""
+    from rcbf_amd.dynamics import DynamicsModel
+    env = types.SimpleNamespace(dynamics_mode="Unicycle", dt=0.02)
+    dm = DynamicsModel(env, types.SimpleNamespace(cuda=True, gp_model_size=1000))
+    rng = np.random.default_rng(12)
+    x = np.stack([rng.uniform(-3, 3, 1000), rng.uniform(-3, 3, 1000), rng.uniform(-np.pi, np.pi, 1000)], 1)
+    u = rng.uniform(-1, 1, (1000, 2))
+    nx = O.predict_next_state_prior("Unicycle", x, u) + 0.02 * (0.05 * np.sin(x) + rng.normal(0, 0.02, x.shape))
+    dm.append_transition(x, u, nx)
+    gpm = dm.disturb_estimators
+    assert gpm.rank == 100 and gpm.love_init is not None and gpm.r <= 100
+    qs = rng.normal(0, 1, (257, 3)).astype(np.float32)
+    mean, std = dm.predict_disturbance(torch.as_tensor(qs, device="cuda"))
+    mo, so = O.gp_predict(qs, dm.train_x, dm.train_y, gpm.hyper, rank=100, love_init=gpm.love_init.numpy())
     _check(mean.cpu().numpy(), std.cpu().numpy(), mo, so)
 
 
@@ -172,7 +222,7 @@ def test_gp_predict_low_rank_split_k():
     model = gp.GPDisturbanceModel(tx, ty, hyper, rank=100)
     q = (rng.normal(0, 1, (256, 3)) * tx.std(0)).astype(np.float32)
     mean, std = model.predict(torch.as_tensor(q, device="cuda"))
-    mo, so = O.gp_predict(q, tx, ty, hyper, rank=100)
+    mo, so = O.gp_predict(q, tx, ty, hyper, rank=100, love_init=model.love_init.numpy())
     _check(mean.cpu().numpy(), std.cpu().numpy(), mo, so)
 
 
