@@ -387,26 +387,35 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
 // posterior is a GEMV per GP, bound by streaming [R | alpha] (rank 100:
 // 10 x 3008 x 128 fp32 = 15.4 MB), so it skips the MFMA tiles (127 of 128
 // query rows would be padding).  ONE launch, r05:
-//  * tile = (GP i, 128-column block cb, 32-column quarter qc, 128 training
-//    rows): every row of a tile is one 128-B line; thread t streams rows
-//    (t >> 3) + 32 j, j < 4, float4 t & 7, its 4 loads issued before it builds
-//    the kernel values k_i(x_b, x_n) of the tile's rows in LDS.  The exact
-//    factor (RCBF_GP_RT_UPPER) only has tiles below 128 (cb + 1).  Rank 100:
-//    10 x 4 x 24 = 960 workgroups; exact N = 3000: 12 000.
-//  * the 32 x BQ partial of a tile goes to the workspace; the last tile of
+//  * tile = (GP i, 128-column block cb, 64 training rows): 32 KB, every row
+//    one whole 512-B line pair; thread t streams rows (t >> 5) + 8 j, j < 8,
+//    float4 t & 31, its 8 loads issued together with the tile's training rows
+//    and queries, so the tile pays one memory round trip; the kernel values
+//    k_i(x_b, x_n) of its rows go through LDS.  The exact factor
+//    (RCBF_GP_RT_UPPER) only has tiles below 128 (cb + 1).  Rank 100:
+//    10 x 47 = 470 workgroups; exact N = 3000: 5 990.
+//  * the 128 x BQ partial of a tile goes to the workspace; the last tile of
 //    block (i, cb) to finish (a per-block arrival counter) sums the block's
 //    partials in a fixed order (deterministic whichever tile is last), forms
-//    sum_{j < r} Q^2 and the mean column; the last block of GP i to finish (a
-//    per-GP counter) writes mean and std.  No combine or finish launch.
+//    sum_{j < r} Q^2 and the mean column, and -- when the GP has one column
+//    block (a Lanczos factor) -- writes mean and std; otherwise the last
+//    block of GP i to finish (a per-GP counter) does.  No combine or finish
+//    launch.
 // The counters live in the first words of the workspace, zero before the
 // first call (the caller zero-fills a new workspace) and reset to zero by the
-// workgroups that consume them.  Release / acquire: every thread fences its
-// partial stores before the workgroup barrier and the arrival atomic; the
-// last workgroup fences again before reading (agent scope: the L2s of the 8
-// XCDs are written back / invalidated by the fences).
-constexpr int kGvRows = 128;  // training rows per tile
-constexpr int kGvCols = 32;   // physical Rt columns per tile (one 128-B line per row)
-constexpr int kGvTiles = kGpCols / kGvCols;  // column quarters per 128-column block
+// workgroups that consume them.  Hand-off (cdna_hip_programming.md §6 G16,
+// MI355X_MICROARCH.md "Valid forms", row 1): every handed-off byte is stored
+// `sc1` (write-through, 16-B tile partials / 4-B block sums), every storing
+// wave drains its stores (`s_waitcnt vmcnt(0)`) before the workgroup barrier
+// behind which ONE lane adds to the arrival counter (relaxed, agent scope),
+// and the workgroup whose add returned the last ticket reads every handed-off
+// byte with `sc1` loads.  No __threadfence: an agent-scope release writes back
+// the whole XCD L2 and an acquire invalidates the CU's L1 (r05b, with them in
+// every workgroup: 72 us for rank 100 at B = 1).
+#ifndef RCBF_GV_ROWS
+#define RCBF_GV_ROWS 64
+#endif
+constexpr int kGvRows = RCBF_GV_ROWS;  // training rows per tile (a tile spans a whole 128-column block)
 
 // tiles of one GP, and where column block cb's tiles start
 __host__ __device__ inline int gp_gv_kend(const rcbf_gp_model& m, int cb) {
@@ -417,18 +426,66 @@ __host__ __device__ inline int gp_gv_rowtiles(const rcbf_gp_model& m, int cb) {
 }
 inline int gp_gv_tiles(const rcbf_gp_model& m) {
     int t = 0;
-    for (int cb = 0; cb < m.C_pad / kGpCols; ++cb) t += kGvTiles * gp_gv_rowtiles(m, cb);
+    for (int cb = 0; cb < m.C_pad / kGpCols; ++cb) t += gp_gv_rowtiles(m, cb);
     return t;
 }
-// counter words at the start of the workspace: n_s * n_cb block counters, then n_s GP counters
+// counter words at the start of the workspace: n_s * n_cb block counters, then n_s GP counters, each
+// on a 128-B line of its own -- arrivals on one line serialise at the memory-side atomic unit (~13 ns
+// each): with the 10 GPs' counters in one line, rank 100 at B = 1 spent ~13 us of its 18 there (r05e)
+constexpr int kGvCtrStride = 32;  // words
 inline int64_t gp_counter_words(const rcbf_gp_model& m) {
-    return ((int64_t)m.n_s * (m.C_pad / kGpCols + 1) + 63) / 64 * 64;
+    return (int64_t)m.n_s * (m.C_pad / kGpCols + 1) * kGvCtrStride;
 }
 
 struct GpCols {
     int32_t n;
     int32_t idx[10];
 };
+
+// the hand-off's loads and 4-B stores: relaxed agent-scope atomics lower to global_load/store ... sc1
+__device__ __forceinline__ float ld_sc1(const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ticket(unsigned* c) {
+    return __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// sum_{r < n} p[r * stride] in order r = 0, 1, ... with sc1 loads, 48 in flight at a time (a load used
+// at once would cost a full memory round trip per term: r05c, 24 terms ~ 20 us)
+__device__ __forceinline__ float sum_sc1(const float* p, int n, int64_t stride) {
+    constexpr int kBatch = 48;
+    float q = 0.0f;
+    for (int r0 = 0; r0 < n; r0 += kBatch) {
+        float a[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) a[u] = ld_sc1(p + (int64_t)min(r0 + u, n - 1) * stride);
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) q += (r0 + u < n) ? a[u] : 0.0f;
+    }
+    return q;
+}
+
+// mean and std of GP i at query b from q = sum_{j < r} Q^2 and the mean column's raw value (the
+// arithmetic of gp_mean_std, dynamics.py:371-380 after gpytorch), into the row and column outputs
+// (os, nz, ys: GP i's outputscale, noise and y_scale, loaded at the kernel's start, off the tail)
+__device__ __forceinline__ void gp_gv_finish(const rcbf_gp_model& m, int64_t B, int i, int b, float q, float mraw,
+                                             float os, float nz, float ys, float* mean_out, float* std_out,
+                                             const GpCols& cols, float* mean_cols, float* std_cols) {
+    const float lat = fmaxf(os - q, 0.0f);  // latent posterior variance
+    const float var = lat + nz;             // likelihood(model(x)).variance
+    const float mu = mraw * ys;
+    const float sd = sqrtf(var) * ys;
+    if (mean_out) mean_out[(int64_t)b * m.n_s + i] = mu;
+    if (std_out) std_out[(int64_t)b * m.n_s + i] = sd;
+    for (int c = 0; c < cols.n; ++c) {
+        if (cols.idx[c] == i) {
+            if (mean_cols) mean_cols[(int64_t)c * B + b] = mu;
+            if (std_cols) std_cols[(int64_t)c * B + b] = sd;
+        }
+    }
+}
 
 template <int D, int BQ>
 __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
@@ -437,115 +494,141 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
                                                  float* __restrict__ std_out, GpCols cols,
                                                  float* __restrict__ mean_cols, float* __restrict__ std_cols) {
     constexpr float kL2E = 1.4426950408889634f;
-    constexpr int RJ = kGvRows / 32;  // rows per thread
+    constexpr int RJ = kGvRows / 8;  // rows per thread
     __shared__ float s_xs[BQ][D];
     __shared__ float s_k[BQ][kGvRows];
-    __shared__ float4 s_red[4][BQ][8];
+    __shared__ float4 s_red[4][BQ][32];
     __shared__ float s_bsum[4][BQ];
+    __shared__ float s_mean[BQ];
     __shared__ int s_last;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int i = blockIdx.y;
     const int n_cb = m.C_pad / kGpCols;
-    // tile -> (cb, rc, qc); tiles are cb-major, then row tile, then quarter
-    int tt = blockIdx.x, cb = 0, base = 0;
+    // tile -> (cb, rc); tiles are cb-major, then row tile
+    int rc = blockIdx.x, cb = 0, base = 0;
     int nrc = gp_gv_rowtiles(m, 0);
-    while (tt >= kGvTiles * nrc) {
-        tt -= kGvTiles * nrc;
-        base += kGvTiles * nrc;
+    while (rc >= nrc) {
+        rc -= nrc;
+        base += nrc;
         ++cb;
         nrc = gp_gv_rowtiles(m, cb);
     }
-    const int rc = tt / kGvTiles, qc = tt % kGvTiles;
     const int n0 = rc * kGvRows;
     const int nrows = min(kGvRows, gp_gv_kend(m, cb) - n0);  // a multiple of 32
     const int64_t ldc = m.C_pad;
 
-    // 1. this thread's Rt values first: rows n0 + (t >> 3) + 32 j, columns cb*128 + qc*32 + 4 (t & 7) ..+3
-    const float* Rp = m.Rt + ((int64_t)i * m.N_pad + n0 + (t >> 3)) * ldc + cb * kGpCols + qc * kGvCols + 4 * (t & 7);
+    // 1. every load of the tile at once -- this thread's 128 B of Rt, then its training row (t < 64)
+    //    and query component (t < BQ D) -- so the whole tile pays one memory round trip.  Rows past
+    //    the tile's end re-read row n0 (in bounds) and get a zero kernel value.
+    const float* Rp = m.Rt + ((int64_t)i * m.N_pad + n0) * ldc + cb * kGpCols + 4 * (t & 31);
     f32x4 v[RJ];
 #pragma unroll
-    for (int j = 0; j < RJ; ++j)
-        v[j] = (32 * j < nrows) ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(Rp + (int64_t)32 * j * ldc))
-                                : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    // 2. the scaled queries (dynamics.py:376: test_x / train_x_std in fp64, then .float())
+    for (int j = 0; j < RJ; ++j) {
+        const int rr = (t >> 5) + 8 * j;
+        v[j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(Rp + (int64_t)(rr < nrows ? rr : 0) * ldc));
+    }
     const float sl = m.inv_sl[i];
-    const float log2s = __log2f(m.outscale[i]);
+    const float os = m.outscale[i], nz = m.noise[i], ys = m.y_scale[i];
+    const float log2s = __log2f(os);
+    float xt[D], tn = 0.0f;
+    {
+        const int n = n0 + (t < nrows ? t : 0);
+#pragma unroll
+        for (int k = 0; k < D; ++k) xt[k] = m.xt[((int64_t)i * m.N_pad + n) * D + k];
+        tn = -kL2E * m.tn2[(int64_t)i * m.N_pad + n];
+    }
+    float xs_raw = 0.0f;
+    double xstd = 1.0;
     if (t < BQ * D) {
         const int b = t / D, k = t % D;
         const int64_t row = b < B ? b : B - 1;
-        s_xs[b][k] = (float)((double)xq[row * D + k] / m.x_std[k]) * sl;
+        xs_raw = xq[row * D + k];
+        xstd = m.x_std[k];
     }
-    __syncthreads();
+    // 2. the scaled queries (dynamics.py:376: test_x / train_x_std in fp64, then .float()).  The barriers
+    //    here are raw s_barrier with an LDS drain only: __syncthreads() would also drain vmcnt, i.e. wait
+    //    for the Rt loads.
+    if (t < BQ * D) s_xs[t / D][t % D] = (float)((double)xs_raw / xstd) * sl;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     // 3. k_i(x_b, x_n) of the tile's rows (the arithmetic of k_gp_qform's level-0 loop)
-    if (t < nrows) {
-        const int n = n0 + t;
-        float xt[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) xt[k] = m.xt[((int64_t)i * m.N_pad + n) * D + k];
-        const float tn = -kL2E * m.tn2[(int64_t)i * m.N_pad + n];
+    if (t < kGvRows) {
 #pragma unroll
         for (int b = 0; b < BQ; ++b) {
-            float nrm = 0.0f;
+            float kv = 0.0f;
+            if (t < nrows) {
+                float nrm = 0.0f;
 #pragma unroll
-            for (int k = 0; k < D; ++k) nrm = fmaf(s_xs[b][k], s_xs[b][k], nrm);
-            float arg = fmaf(-kL2E, nrm, log2s) + tn;
+                for (int k = 0; k < D; ++k) nrm = fmaf(s_xs[b][k], s_xs[b][k], nrm);
+                float arg = fmaf(-kL2E, nrm, log2s) + tn;
 #pragma unroll
-            for (int k = 0; k < D; ++k) arg = fmaf(2.0f * kL2E * s_xs[b][k], xt[k], arg);
-            s_k[b][t] = __builtin_amdgcn_exp2f(fminf(arg, log2s));
+                for (int k = 0; k < D; ++k) arg = fmaf(2.0f * kL2E * s_xs[b][k], xt[k], arg);
+                kv = __builtin_amdgcn_exp2f(fminf(arg, log2s));
+            }
+            s_k[b][t] = kv;
         }
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     // 4. this thread's rows into 4 columns x BQ queries
     float4 acc[BQ];
 #pragma unroll
     for (int b = 0; b < BQ; ++b) acc[b] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
-        if (32 * j < nrows) {
-#pragma unroll
-            for (int b = 0; b < BQ; ++b) {
-                const float kv = s_k[b][(t >> 3) + 32 * j];
-                acc[b].x = fmaf(kv, v[j][0], acc[b].x);
-                acc[b].y = fmaf(kv, v[j][1], acc[b].y);
-                acc[b].z = fmaf(kv, v[j][2], acc[b].z);
-                acc[b].w = fmaf(kv, v[j][3], acc[b].w);
-            }
-        }
-    }
-    // 5. sum over the 8 row groups of a wave (lane bits 3..5), then over the 4 waves
-#pragma unroll
-    for (int msk = 8; msk < 64; msk <<= 1) {
 #pragma unroll
         for (int b = 0; b < BQ; ++b) {
-            acc[b].x += __shfl_xor(acc[b].x, msk, 64);
-            acc[b].y += __shfl_xor(acc[b].y, msk, 64);
-            acc[b].z += __shfl_xor(acc[b].z, msk, 64);
-            acc[b].w += __shfl_xor(acc[b].w, msk, 64);
+            const float kv = s_k[b][(t >> 5) + 8 * j];
+            acc[b].x = fmaf(kv, v[j][0], acc[b].x);
+            acc[b].y = fmaf(kv, v[j][1], acc[b].y);
+            acc[b].z = fmaf(kv, v[j][2], acc[b].z);
+            acc[b].w = fmaf(kv, v[j][3], acc[b].w);
         }
     }
-    if (lane < 8) {
+#if defined(RCBF_GV_STUDY) && RCBF_GV_STUDY == 3  // study: the tile's loads and FMAs only
+    {
+        float z = 0.0f;
+#pragma unroll
+        for (int b = 0; b < BQ; ++b) z += acc[b].x + acc[b].y + acc[b].z + acc[b].w;
+        if (z == 1.2345f) part[t] = z;
+    }
+    return;
+#endif
+    // 5. sum the wave's two row groups (lane bit 5), then the 4 waves through LDS
+#pragma unroll
+    for (int b = 0; b < BQ; ++b) {
+        acc[b].x += __shfl_xor(acc[b].x, 32, 64);
+        acc[b].y += __shfl_xor(acc[b].y, 32, 64);
+        acc[b].z += __shfl_xor(acc[b].z, 32, 64);
+        acc[b].w += __shfl_xor(acc[b].w, 32, 64);
+    }
+    if (lane < 32) {
 #pragma unroll
         for (int b = 0; b < BQ; ++b) s_red[w][b][lane] = acc[b];
     }
     __syncthreads();
-    const int tile = base + tt;
-    if (t < 8 * BQ) {
-        const int b = t >> 3, f = t & 7;
+    const int tile = base + rc;
+    if (t < 32 * BQ) {
+        const int b = t >> 5, f = t & 31;
         float4 a = s_red[0][b][f];
 #pragma unroll
         for (int u = 1; u < 4; ++u) {
             const float4 o = s_red[u][b][f];
             a.x += o.x, a.y += o.y, a.z += o.z, a.w += o.w;
         }
-        reinterpret_cast<float4*>(part)[(((int64_t)i * T + tile) * BQ + b) * (kGvCols / 4) + f] = a;
+        st_out4<true>(part + (((int64_t)i * T + tile) * BQ + b) * kGpCols + 4 * f, a);  // sc1
     }
+#if defined(RCBF_GV_STUDY) && RCBF_GV_STUDY == 1  // study: no hand-off (partials stored, no arrival)
+    return;
+#endif
     // 6. arrival at block (i, cb): the last of its tiles reduces the block
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t == 0) s_last = atomicAdd(&counters[i * n_cb + cb], 1u) == (unsigned)(kGvTiles * nrc - 1);
+    if (t == 0) s_last = ticket(&counters[(i * n_cb + cb) * kGvCtrStride]) == (unsigned)(nrc - 1);
     __syncthreads();
     if (!s_last) return;
-    __threadfence();
     const int r_rank = m.r;
     // thread t: physical column p = t & 127 of the block, queries b = (t >> 7), (t >> 7) + 2, ...
     const int p = t & 127;
@@ -556,9 +639,11 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
         const int b = (t >> 7) + 2 * h;
         float q = 0.0f;
         if (b < BQ) {
-            const float* pp = part + (((int64_t)i * T + base + (p >> 5)) * BQ + b) * kGvCols + (p & 31);
-            for (int r = 0; r < nrc; ++r) q += pp[(int64_t)r * kGvTiles * BQ * kGvCols];
-            if (lc == r_rank && b < B) meanraw[(int64_t)i * BQ + b] = q;
+            q = sum_sc1(part + (((int64_t)i * T + base) * BQ + b) * kGpCols + p, nrc, (int64_t)BQ * kGpCols);
+            if (lc == r_rank && b < B) {
+                st_sc1(meanraw + (int64_t)i * BQ + b, q);
+                s_mean[b] = q;
+            }
         }
         vq[h] = (lc < r_rank) ? q * q : 0.0f;
     }
@@ -570,38 +655,32 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
         if (lane == 0 && (t >> 7) + 2 * h < BQ) s_bsum[w][h] = x;
     }
     __syncthreads();
+    if (n_cb == 1) {  // the block is the whole GP (a Lanczos factor): finish here, no second hand-off
+        if (t < B) {
+            const int h = t >> 1, w0 = (t & 1) * 2;
+            gp_gv_finish(m, B, i, t, 0.0f + (s_bsum[w0][h] + s_bsum[w0 + 1][h]), s_mean[t], os, nz, ys, mean_out,
+                         std_out, cols, mean_cols, std_cols);
+        }
+        if (t == 0) atomicExch(&counters[(i * n_cb + cb) * kGvCtrStride], 0u);
+        return;
+    }
     if (t < BQ) {  // query b = t: waves 0, 1 hold even b (slot b / 2), waves 2, 3 odd b
         const int h = t >> 1, w0 = (t & 1) * 2;
-        blk[((int64_t)i * n_cb + cb) * BQ + t] = s_bsum[w0][h] + s_bsum[w0 + 1][h];
+        st_sc1(blk + ((int64_t)i * n_cb + cb) * BQ + t, s_bsum[w0][h] + s_bsum[w0 + 1][h]);
     }
     // 7. arrival at GP i: the last of its blocks writes mean and std
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
-        atomicExch(&counters[i * n_cb + cb], 0u);  // consumed: zero for the next call
-        s_last = atomicAdd(&counters[m.n_s * n_cb + i], 1u) == (unsigned)(n_cb - 1);
+        atomicExch(&counters[(i * n_cb + cb) * kGvCtrStride], 0u);  // consumed: zero for the next call
+        s_last = ticket(&counters[(m.n_s * n_cb + i) * kGvCtrStride]) == (unsigned)(n_cb - 1);
     }
     __syncthreads();
     if (!s_last) return;
-    __threadfence();
-    if (t < B) {
-        const int b = t;
-        float q = 0.0f;
-        for (int c = 0; c < n_cb; ++c) q += blk[((int64_t)i * n_cb + c) * BQ + b];
-        const float lat = fmaxf(m.outscale[i] - q, 0.0f);  // latent posterior variance
-        const float var = lat + m.noise[i];                  // likelihood(model(x)).variance
-        const float mu = meanraw[(int64_t)i * BQ + b] * m.y_scale[i];
-        const float sd = sqrtf(var) * m.y_scale[i];
-        if (mean_out) mean_out[(int64_t)b * m.n_s + i] = mu;
-        if (std_out) std_out[(int64_t)b * m.n_s + i] = sd;
-        for (int c = 0; c < cols.n; ++c) {
-            if (cols.idx[c] == i) {
-                if (mean_cols) mean_cols[(int64_t)c * B + b] = mu;
-                if (std_cols) std_cols[(int64_t)c * B + b] = sd;
-            }
-        }
-    }
-    if (t == 0) atomicExch(&counters[m.n_s * n_cb + i], 0u);
+    if (t < B)
+        gp_gv_finish(m, B, i, t, sum_sc1(blk + (int64_t)i * n_cb * BQ + t, n_cb, BQ),
+                     ld_sc1(meanraw + (int64_t)i * BQ + t), os, nz, ys, mean_out, std_out, cols, mean_cols, std_cols);
+    if (t == 0) atomicExch(&counters[(m.n_s * n_cb + i) * kGvCtrStride], 0u);
 }
 
 // Split-K combine (the MFMA path, B > 8): one wave per (GP i, column block
@@ -705,7 +784,7 @@ int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B) {
     const int64_t n_cb = m->C_pad / kGpCols;
     const int64_t cw = gp_counter_words(*m);
     if (B <= kGvMaxB)  // GEMV: tile partials (32 columns x 8 queries), block sums, mean column
-        return cw + (int64_t)m->n_s * gp_gv_tiles(*m) * kGvMaxB * kGvCols + (int64_t)m->n_s * (n_cb + 1) * kGvMaxB;
+        return cw + (int64_t)m->n_s * gp_gv_tiles(*m) * kGvMaxB * kGpCols + (int64_t)m->n_s * (n_cb + 1) * kGvMaxB;
     const int sk = gp_split(m, B);
     // partials for up to 2 launches per block, + means, + the split-K raw Q tiles
     return cw + (int64_t)m->n_s * (2 * n_cb + 1) * B + (sk > 1 ? (int64_t)sk * m->n_s * B * m->C_pad : 0);
@@ -743,7 +822,7 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
     if (B <= kGvMaxB) {
         const int T = gp_gv_tiles(*m);
         float* part = ws;
-        float* blk = part + (int64_t)m->n_s * T * kGvMaxB * kGvCols;
+        float* blk = part + (int64_t)m->n_s * T * kGvMaxB * kGpCols;
         float* mraw = blk + (int64_t)m->n_s * n_cb * kGvMaxB;
         dim3 gv((unsigned)T, (unsigned)m->n_s);
 #define RCBF_GV_L(DD, BB)                                                                                  \

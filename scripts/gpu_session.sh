@@ -109,6 +109,11 @@ for step in "$@"; do
       done; done ;;
     gpt)    run gpt 600 python -u -m pytest tests/test_gpu_gp.py tests/test_gpu_parity.py -q -rf --timeout 300 --timeout-method thread ;;
     gpgb)   run gpgb 300 python -u scripts/gp_graph_bench.py ;;
+    gvstudy)  # GEMV study variants (build/variants/librcbf_gv*.so) vs the product, GP graph bench
+      for n in prod gv1 gv3 gvr128; do
+        if [ "$n" = prod ]; then lib=""; else lib="RCBF_HIP_LIB=build/variants/librcbf_$n.so"; fi
+        env $lib timeout -k 10 200 python scripts/gp_graph_bench.py > "$OUT/gvstudy_$n.log" 2>&1 || exit 1
+      done ;;
     profgp) run profgp 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profgp" -o run -- \
               python3 scripts/gp_graph_bench.py 20 5
       [ -f "$OUT/profgp/run_kernel_stats.csv" ] && cp "$OUT/profgp/run_kernel_stats.csv" "$OUT/kernel_stats_gp_graph_bench_$TAG.csv" ;;
