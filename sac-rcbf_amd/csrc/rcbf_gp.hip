@@ -687,9 +687,18 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
 // cb, query b) adds the n_split raw Q rows (fixed order) over the block's 128
 // columns, then partial = sum_{col < r} Q^2 and meanraw = Q(b, r), as
 // k_gp_qform's own epilogue.
+// fin (one column block per GP, a Lanczos factor): the wave also finishes its
+// query -- mean and std into the row and column outputs, the arithmetic of
+// gp_mean_std -- so no finish launch follows.
+__device__ __forceinline__ void gp_gv_finish(const rcbf_gp_model& m, int64_t B, int i, int b, float q, float mraw,
+                                             float os, float nz, float ys, float* mean_out, float* std_out,
+                                             const GpCols& cols, float* mean_cols, float* std_cols);
+
 __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, int n_cb, int n_split,
                                                     const float* __restrict__ qraw, float* __restrict__ partial,
-                                                    float* __restrict__ meanraw) {
+                                                    float* __restrict__ meanraw, int fin, float* __restrict__ mean_out,
+                                                    float* __restrict__ std_out, GpCols cols,
+                                                    float* __restrict__ mean_cols, float* __restrict__ std_cols) {
     const int64_t wv = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (wv >= (int64_t)m.n_s * n_cb * B) return;
@@ -697,17 +706,38 @@ __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, 
     const int cb = (int)((wv / B) % n_cb);
     const int i = (int)(wv / (B * n_cb));
     const int64_t ldc = m.C_pad;
-    float v = 0.0f;
+    float v = 0.0f, mq = 0.0f;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int col = cb * kGpCols + 64 * h + lane;  // logical column: k_gp_qform stores Q by logical column
+        // the n_split terms in order, 16 loads in flight at a time (a loop that adds each load as it
+        // arrives pays a memory round trip per split: r05i, 11 splits ~ 9 us)
+        const float* qp = qraw + ((int64_t)i * n_split * B + b) * ldc + col;
+        const int64_t qs = B * ldc;
         float q = 0.0f;
-        for (int s = 0; s < n_split; ++s) q += qraw[(((int64_t)i * n_split + s) * B + b) * ldc + col];
+        for (int s0 = 0; s0 < n_split; s0 += 16) {
+            float a[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) a[u] = qp[(int64_t)min(s0 + u, n_split - 1) * qs];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) q += (s0 + u < n_split) ? a[u] : 0.0f;
+        }
         v += (col < m.r) ? q * q : 0.0f;
-        if (col == m.r) meanraw[(int64_t)i * B + b] = q;
+        if (col == m.r) {
+            meanraw[(int64_t)i * B + b] = q;
+            mq = q;
+        }
     }
 #pragma unroll
     for (int msk = 1; msk < 64; msk <<= 1) v += __shfl_xor(v, msk, 64);
+    if (fin) {  // n_cb == 1: this wave saw every column of GP i at query b
+#pragma unroll
+        for (int msk = 1; msk < 64; msk <<= 1) mq += __shfl_xor(mq, msk, 64);  // the one lane holding column r
+        if (lane == 0)
+            gp_gv_finish(m, B, i, (int)b, 0.0f + v, mq, m.outscale[i], m.noise[i], m.y_scale[i], mean_out, std_out,
+                         cols, mean_cols, std_cols);
+        return;
+    }
     if (lane == 0) partial[((int64_t)i * n_cb + cb) * B + b] = v;
 }
 
@@ -717,8 +747,15 @@ __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, 
 // mean and std of GP i at query b (dynamics.py:371-380 after gpytorch)
 __device__ __forceinline__ void gp_mean_std(const rcbf_gp_model& m, int64_t B, int n_cb, const float* partial,
                                             const float* meanraw, int i, int64_t b, float& mu, float& sd) {
-    float q = 0.0f;
-    for (int c = 0; c < n_cb; ++c) q += partial[((int64_t)i * n_cb + c) * B + b];
+    float q = 0.0f;  // the n_cb block sums in order, 16 loads in flight at a time
+    const float* pp = partial + (int64_t)i * n_cb * B + b;
+    for (int c0 = 0; c0 < n_cb; c0 += 16) {
+        float a[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) a[u] = pp[(int64_t)min(c0 + u, n_cb - 1) * B];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) q += (c0 + u < n_cb) ? a[u] : 0.0f;
+    }
     const float lat = fmaxf(m.outscale[i] - q, 0.0f);  // latent posterior variance
     const float var = lat + m.noise[i];                  // likelihood(model(x)).variance
     mu = meanraw[(int64_t)i * B + b] * m.y_scale[i];
@@ -885,8 +922,10 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
     }
     if (sk > 1) {
         const int64_t waves = (int64_t)m->n_s * n_cb * B;
+        const int fin = n_cb == 1;  // a Lanczos factor: the combine also finishes (no k_gp_finish launch)
         hipLaunchKernelGGL(k_gp_combine, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, *m, B, n_cb, sk,
-                           qraw, partial, meanraw);
+                           qraw, partial, meanraw, fin, mean_out, std_out, gc, mean_cols, std_cols);
+        if (fin) return launch_status();
     }
     if (mean_out || std_out) {
         const int64_t tot = B * m->n_s;

@@ -48,7 +48,11 @@ def main():
     ty = 0.1 * np.sin(tx) + rng.normal(0, 0.05, (3000, 10))
     hyper = [(1.5, 0.2, 0.05)] * 10
     out = {}
+    only = os.environ.get("GP_BENCH_ONLY", "")  # e.g. "love100:256" -- one model (and batch) for a clean trace
+    om, _, ob = only.partition(":")
     for name, rank in (("love100", 100), ("exact", None)):
+        if om and name != om:
+            continue
         m = gp.GPDisturbanceModel(tx, ty, hyper, device="cuda", rank=rank)
         if rank is None:
             rows = sum(min(m.N, 128 * (cb + 1)) for cb in range(m._m.C_pad // 128))
@@ -56,6 +60,8 @@ def main():
         else:
             rt_bytes = m._m.N_pad * m._m.C_pad * 4 * 10
         for B in (1, 2, 8, 256, 4096):
+            if ob and B != int(ob):
+                continue
             x = torch.as_tensor(rng.normal(0, 1, (B, 10)), dtype=torch.float32, device="cuda")
             ms = time_graph(lambda: m.predict(x), rs if B <= 256 else rl)
             rec = {"us": round(ms * 1e3, 2), "tflops": round(m.flops_per_query() * B / ms / 1e9, 2)}

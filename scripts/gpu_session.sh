@@ -108,12 +108,19 @@ for step in "$@"; do
         echo "$n $(tail -1 "$OUT/gp_${n}_$r.log")" >> "$OUT/gpab_sum.txt"
       done; done ;;
     gpt)    run gpt 600 python -u -m pytest tests/test_gpu_gp.py tests/test_gpu_parity.py -q -rf --timeout 300 --timeout-method thread ;;
+    loop)   run loop 900 python -u -m pytest tests/test_gpu_training_loop.py -q -rf -s --timeout 600 --timeout-method thread ;;
     gpgb)   run gpgb 300 python -u scripts/gp_graph_bench.py ;;
     gvstudy)  # GEMV study variants (build/variants/librcbf_gv*.so) vs the product, GP graph bench
       for n in prod gv1 gv3 gvr128; do
         if [ "$n" = prod ]; then lib=""; else lib="RCBF_HIP_LIB=build/variants/librcbf_$n.so"; fi
         env $lib timeout -k 10 200 python scripts/gp_graph_bench.py > "$OUT/gvstudy_$n.log" 2>&1 || exit 1
       done ;;
+    profgp256) GP_BENCH_ONLY=love100:256 run profgp256 300 rocprofv3 --kernel-trace --stats --output-format csv \
+              -d "$OUT/profgp256" -o run -- python3 scripts/gp_graph_bench.py 20 5
+      [ -f "$OUT/profgp256/run_kernel_stats.csv" ] && cp "$OUT/profgp256/run_kernel_stats.csv" "$OUT/kernel_stats_gp_love100_B256_$TAG.csv" ;;
+    profgp1) GP_BENCH_ONLY=love100:1 run profgp1 300 rocprofv3 --kernel-trace --stats --output-format csv \
+              -d "$OUT/profgp1" -o run -- python3 scripts/gp_graph_bench.py 20 5
+      [ -f "$OUT/profgp1/run_kernel_stats.csv" ] && cp "$OUT/profgp1/run_kernel_stats.csv" "$OUT/kernel_stats_gp_love100_B1_$TAG.csv" ;;
     profgp) run profgp 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profgp" -o run -- \
               python3 scripts/gp_graph_bench.py 20 5
       [ -f "$OUT/profgp/run_kernel_stats.csv" ] && cp "$OUT/profgp/run_kernel_stats.csv" "$OUT/kernel_stats_gp_graph_bench_$TAG.csv" ;;
