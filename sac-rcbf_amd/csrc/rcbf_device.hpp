@@ -1514,6 +1514,46 @@ __device__ __forceinline__ void uni_qp_2d_core(double p0, double p1, double p2, 
     if (!finite) z[0] = z[1] = z[2] = __builtin_nan("");
 }
 
+// uni_qp_2d_core's solve from a live-row mask computed elsewhere: the
+// lane-pair STUDY build (csrc/study/rcbf_uni_pair.hip) forms the mask from the
+// two lanes' halves of the hazard rows.  The product inlines uni_qp_2d_core
+// (kept unchanged, so its machine code is untouched).
+template <int K, typename T>
+__device__ __forceinline__ void uni_qp_2d_masked(double p0, double p1, double p2, double ip0, double ip1,
+                                                 const T* a0, const T* a1, const T* b, unsigned mask, double L0,
+                                                 double U0, double L1, double U1, bool finite, double* z, int& status) {
+    double bu0, bu1, bf, e;
+    const int kmax = wave_max_count<K>(__popc(mask));
+    RCBF_QP_COUNT(8, kmax > 0);
+    RCBF_QP_COUNT(10, kmax > 1);
+    RCBF_QP_COUNT(11, kmax > 2);
+    if (kmax == 0) {  // no hazard row can bind anywhere in the box, for every lane of the wave
+        bu0 = fmin(fmax(0.0, L0), U0);
+        bu1 = fmin(fmax(0.0, L1), U1);
+        bf = 0.0;
+        e = 0.0;
+    } else if (kmax == 1 || K == 1) {
+        uni_slots_solve<1, K, T>(p0, p1, p2, ip0, ip1, a0, a1, b, mask, L0, U0, L1, U1, bu0, bu1, bf, e);
+    } else if (kmax == 2 || K == 2) {
+        uni_slots_solve<(K >= 2 ? 2 : 1), K, T>(p0, p1, p2, ip0, ip1, a0, a1, b, mask, L0, U0, L1, U1, bu0, bu1,
+                                                bf, e);
+    } else if (kmax == 3 || K == 3) {
+        uni_slots_solve<(K >= 3 ? 3 : 1), K, T>(p0, p1, p2, ip0, ip1, a0, a1, b, mask, L0, U0, L1, U1, bu0, bu1,
+                                                bf, e);
+    } else {
+        uni_slots_solve<K, K, T>(p0, p1, p2, ip0, ip1, a0, a1, b, mask, L0, U0, L1, U1, bu0, bu1, bf, e);
+    }
+    z[0] = bu0;
+    z[1] = bu1;
+    z[2] = e;
+    RCBF_QP_STAMP(9);
+    finite = finite && isfinite(U0 + L0 + U1 + L1);  // fmin/fmax would hide a NaN bound
+    const bool ok = isfinite(z[0]) && isfinite(z[1]) && isfinite(z[2]) && bf < __builtin_huge_val();
+    status = !finite ? RCBF_QP_NONFINITE : (ok && L0 <= U0 && L1 <= U1 ? RCBF_QP_OK : RCBF_QP_INFEASIBLE);
+    if (!finite) z[0] = z[1] = z[2] = __builtin_nan("");
+}
+
+
 // On the normalised rows (what qpth sees): back to the slack form by one
 // division per row by its (negative) slack coefficient.
 template <int K, typename R>

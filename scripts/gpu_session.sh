@@ -96,6 +96,20 @@ for step in "$@"; do
         --output-format csv -d "$OUT/sq_$wl" -o run -- python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 $(wl_args "$wl")
       [ -f "$OUT/sq_$wl/run_counter_collection.csv" ] && python scripts/pmc_sq.py "$OUT/sq_$wl/run_counter_collection.csv" \
         "$(wl_kernel "$wl")" > "$OUT/pmc_sq_$(wl_name "$wl").txt" ;;
+    if_*)  # instruction-fetch waits: SQ wave-cycle shares and instruction-cache misses, one pass
+      run "if_$wl" 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_IFETCH SQ_INSTS_VALU SQC_ICACHE_MISSES \
+        --output-format csv -d "$OUT/if_$wl" -o run -- python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 $(wl_args "$wl")
+      [ -f "$OUT/if_$wl/run_counter_collection.csv" ] && python scripts/pmc_sq.py "$OUT/if_$wl/run_counter_collection.csv" \
+        "$(wl_kernel "$wl")" > "$OUT/pmc_ifetch_$(wl_name "$wl").txt" ;;
+    pair)  # the unicycle lane-pair study build vs the product (scripts/uni_pair_study.py)
+      run pair 300 python -u scripts/uni_pair_study.py
+      RCBF_PAIR_VARIANT=core run pair_core 300 python -u scripts/uni_pair_study.py ;;
+    pairsq)
+      RCBF_PAIR_VARIANT=core run pairsq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU \
+        --output-format csv -d "$OUT/pairsq" -o run -- python3 scripts/uni_pair_study.py --sq
+      [ -f "$OUT/pairsq/run_counter_collection.csv" ] && for kk in "k_uni_pair_step<5, 256>" "k_safe_step<0, 1, 5, false, 256, false>" \
+          "k_uni_pair_step<3, 64>" "k_uni_pair_step<3, 128>" "k_safe_step<0, 1, 3, false, 64, false>"; do
+        echo "== $kk" >> "$OUT/pmc_sq_pair.txt"; python scripts/pmc_sq.py "$OUT/pairsq/run_counter_collection.csv" "$kk" >> "$OUT/pmc_sq_pair.txt"; done ;;
     tracer)  # control: torch kernels of the same bytes, untraced (events) and traced
       run tracer_plain 120 python scripts/tracer_control.py
       run tracer_traced 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/tracer" -o run -- \
