@@ -268,3 +268,47 @@ def test_gp_predict_cols_equals_rows(n_s, cols, B):
         runs.append([obs.clone(), r.clone(), o["u"].clone(), env.state.clone()])
     for a, b in zip(*runs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rank", [100, None])
+def test_gp_gemv_handoff_across_calls(rank):
+    """The one-launch GEMV (B <= 8) hands its tile partials to the last
+    arriving workgroup through write-through stores and arrival counters that
+    the consumers reset: 48 back-to-back calls on one workspace, each with
+    its own queries (B cycling 1, 2, 3, 8), captured in one hipGraph, every
+    output against the oracle -- a stale partial or a counter left non-zero
+    would reuse an earlier call's values.  The counters are zero afterwards."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(77 + (rank or 0))
+    tx, ty = _data(rng, 1500, 10)
+    hyper = [(rng.uniform(0.8, 2.5), rng.uniform(0.05, 0.5), rng.uniform(0.01, 0.2)) for _ in range(10)]
+    model = gp.GPDisturbanceModel(tx, ty, hyper, rank=rank)
+    sizes = [(1, 2, 3, 8)[j % 4] for j in range(48)]
+    q = (rng.normal(0, 1, (sum(sizes), 10)) * tx.std(0)).astype(np.float32)
+    qd = torch.as_tensor(q, device="cuda")
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    model.predict(qd[:8].contiguous())  # size the workspace for B = 8 before the capture
+    xs = [qd[offs[j]:offs[j + 1]].clone() for j in range(48)]
+    outs = [(torch.empty(sizes[j], 10, device="cuda"), torch.empty(sizes[j], 10, device="cuda")) for j in range(48)]
+    import ctypes
+    from rcbf_amd import _lib
+    lib = _lib.load()
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for j in range(48):
+            rc = lib.rcbf_gp_predict(ctypes.byref(model._m), sizes[j], _lib.ptr(xs[j]), _lib.ptr(outs[j][0]),
+                                     _lib.ptr(outs[j][1]), _lib.ptr(model._ws), _lib.stream_of(torch.device("cuda")))
+            assert rc == 0
+    mo, so = O.gp_predict(q, tx, ty, hyper, rank=rank, love_init=None if rank is None else model.love_init.numpy())
+    for _ in range(2):
+        for o in outs:
+            o[0].zero_()
+            o[1].zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        for j in range(48):
+            _check(outs[j][0].cpu().numpy(), outs[j][1].cpu().numpy(), mo[offs[j]:offs[j + 1]], so[offs[j]:offs[j + 1]])
+    # the arrival counters (one per 128-B line: n_s (n_cb + 1) of them) lead the workspace and are zero again
+    n_ctr = model.n_s * (model._m.C_pad // 128 + 1) * 32
+    assert int(model._ws.view(torch.int32)[:n_ctr].abs().sum()) == 0
