@@ -293,6 +293,15 @@ int rcbf_predict_next_state(const rcbf_params* prm, int64_t B, const double* x, 
                             const double* t, const float* mean, const float* std, int32_t use_gps,
                             double* next_x, double* std_out, double* next_t, hipStream_t stream);
 
+/* DynamicsModel.get_state (rcbf_sac/dynamics.py:190-232) on fp32
+ * observation rows, one launch: obs (B, n_o) f32 -> state (B, n_s) f32 with
+ * the reference's arithmetic (to numpy fp64, cars x100 / x30, unicycle
+ * arctan2(sin, cos), back to fp32) -- the state that rcbf_obs_safe_action
+ * builds in-kernel, for the GP query of RCBF_SAC.get_safe_action
+ * (sac_cbf.py:233-236). */
+int rcbf_state_from_obs(const rcbf_params* prm, int64_t B, const float* obs, float* state_out,
+                        hipStream_t stream);
+
 /* ReplayMemory.batch_push (replay_memory.py:23-29) as one launch: n records
  * of W f64 (state, action, reward, next_state, mask, t, next_t packed) into
  * the ring of `cap` records starting at record `pos` (wrapping). */

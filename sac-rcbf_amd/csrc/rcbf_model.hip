@@ -219,6 +219,22 @@ __global__ void __launch_bounds__(256) k_gather_rows(double* __restrict__ dst, c
 
 }  // namespace
 
+// DynamicsModel.get_state on fp32 observation rows (dynamics.py:190-232): the
+// state rcbf_obs_safe_action forms in-kernel (state_from_obs32), one row per thread
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) k_state_from_obs(int64_t B, const float* __restrict__ obs,
+                                                           float* __restrict__ state) {
+    using D = Dims<MODE, 1>;
+    const int64_t i = env_index();
+    if (i >= B) return;
+    float o[D::NO], s32[D::NS];
+#pragma unroll
+    for (int k = 0; k < D::NO; ++k) o[k] = obs[i * D::NO + k];
+    state_from_obs32<MODE>(o, s32);
+#pragma unroll
+    for (int k = 0; k < D::NS; ++k) state[i * D::NS + k] = s32[k];
+}
+
 extern "C" {
 
 int rcbf_model_step(const rcbf_params* prm, int64_t B, const double* obs, const double* act, const double* t,
@@ -255,6 +271,20 @@ int rcbf_predict_next_state(const rcbf_params* prm, int64_t B, const double* x, 
     else
         hipLaunchKernelGGL((k_predict_next_state<RCBF_MODE_UNICYCLE>), g, b, 0, stream, B, x, act, t, mean, stdv,
                            (int)use_gps, next_x, std_out, next_t);
+    return launch_status();
+}
+
+int rcbf_state_from_obs(const rcbf_params* prm, int64_t B, const float* obs, float* state_out, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (B < 0) return RCBF_E_BAD_SHAPE;
+    if (B == 0) return 0;
+    if (!obs || !state_out) return RCBF_E_NULL;
+    if (prm->mode == RCBF_MODE_SIMULATED_CARS)
+        hipLaunchKernelGGL((k_state_from_obs<RCBF_MODE_SIMULATED_CARS>), dim3(grid_for(B)), dim3(kBlock), 0, stream, B,
+                           obs, state_out);
+    else
+        hipLaunchKernelGGL((k_state_from_obs<RCBF_MODE_UNICYCLE>), dim3(grid_for(B)), dim3(kBlock), 0, stream, B, obs,
+                           state_out);
     return launch_status();
 }
 

@@ -87,6 +87,7 @@ SIGNATURES = {
     "rcbf_gp_workspace_floats": [_GPM, _I64],
     "rcbf_predict_next_state": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P],
     "rcbf_model_step": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _U64, _U64, _P, _P, _P, _P, _P],
+    "rcbf_state_from_obs": [_PRM, _I64, _P, _P, _P],
     "rcbf_ring_scatter_f64": [_P, _I64, _I64, _I64, _P, _I64, _P],
     "rcbf_gather_rows_f64": [_P, _P, _I64, _P, _I64, _P],
     "rcbf_gp_predict": [_GPM, _I64, _P, _P, _P, _P, _P],

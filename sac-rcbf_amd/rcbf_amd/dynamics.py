@@ -147,8 +147,31 @@ class DynamicsModel:
             torch.cuda.manual_seed(s)
 
     # -- obs <-> state (dynamics.py:190-261) -------------------------------
+    def _state_from_obs_device(self, obs):
+        """fp32 observation rows on the device -> fp32 state rows in ONE launch
+        (rcbf_state_from_obs: the reference's fp64 rescale / arctan2, then fp32,
+        the state rcbf_obs_safe_action forms in-kernel)."""
+        import ctypes
+        from . import _lib
+        from .params import mode_id
+        prm = getattr(self, "_prm_state", None)
+        if prm is None:  # get_state reads only the mode (the hazard count just has to be valid)
+            prm = self._prm_state = _lib.RcbfParams()
+            prm.mode = mode_id(self.env.dynamics_mode)
+            prm.num_hazards = 1 if prm.mode == _lib.MODE_UNICYCLE else 0
+        o = obs.contiguous()
+        out = torch.empty(o.shape[0], self.n_s, dtype=torch.float32, device=o.device)
+        rc = _lib.load().rcbf_state_from_obs(ctypes.byref(prm), o.shape[0], _lib.ptr(o), _lib.ptr(out),
+                                             _lib.stream_of(o.device))
+        _lib.check(rc, "rcbf_state_from_obs")
+        return out
+
     def get_state(self, obs):
         expand = len(obs.shape) == 1
+        if torch.is_tensor(obs) and obs.is_cuda and obs.dtype == torch.float32:
+            o = obs.unsqueeze(0) if expand else obs
+            s = self._state_from_obs_device(o)
+            return s.squeeze(0) if expand else s
         if torch.is_tensor(obs):
             o = obs.unsqueeze(0) if expand else obs
             # the reference rescales in fp64 numpy then casts back to obs.dtype

@@ -7,8 +7,9 @@ obs -> numpy -> get_state -> predict_disturbance (numpy) -> torch ->
 CBFQPLayer, two host round trips per call (dynamics.py:205-232, 357-390).
 Here the prior-disturbance case is ONE kernel (rcbf_obs_safe_action:
 get_state + rows + normalise + exact QP + clamp) and its backward one more;
-with a fitted GP disturbance model the state and the GP posterior stay on
-the device and feed CBFQPLayer.get_safe_action.
+with a fitted GP disturbance model, three launches: rcbf_state_from_obs (the
+GP's query state), rcbf_gp_predict (the posterior) and the same safe-action
+kernel reading the per-env mean / sigma rows.
 """
 import torch
 
@@ -21,7 +22,8 @@ def get_safe_action(cbf_layer, obs_batch, action_batch, dynamics_model):
     differentiable w.r.t. action_batch."""
     if not isinstance(cbf_layer, CBFQPLayer):
         raise TypeError("cbf_layer must be an rcbf_amd CBFQPLayer")
-    if getattr(dynamics_model, "disturb_estimators", None):
+    gpm = getattr(dynamics_model, "disturb_estimators", None)
+    if gpm and not hasattr(gpm, "predict"):  # not rcbf_amd's GP model: the reference's three calls
         state = dynamics_model.get_state(obs_batch)
         mean, sigma = dynamics_model.predict_disturbance(state)
         return cbf_layer.get_safe_action(state, action_batch, mean, sigma)
@@ -41,7 +43,14 @@ def get_safe_action(cbf_layer, obs_batch, action_batch, dynamics_model):
     if obs.dim() != 2 or obs.shape[1] != n_o or u.shape != (obs.shape[0], cbf_layer.action_dim):
         raise ValueError(f"expected obs (B,{n_o}) and action (B,{cbf_layer.action_dim}), got "
                          f"{tuple(obs.shape)} / {tuple(u.shape)}")
-    out = safe_action_op(cbf_layer, obs, u, None, None, True)
+    mean = sigma = None
+    if gpm:
+        # with the GP fitted (dynamics.py:342-390): the state from the observation (rcbf_state_from_obs, the
+        # state the safe-action kernel forms itself), the GP posterior on it (rcbf_gp_predict), then the same
+        # one-launch safe action reading the per-env mean / sigma rows -- three launches, no host round trip
+        state = dynamics_model.get_state(obs)
+        mean, sigma = gpm.predict(state)
+    out = safe_action_op(cbf_layer, obs, u, mean, sigma, True)
     if out.device != out_device:
         out = out.to(out_device)
     return out.squeeze(0) if expand else out

@@ -312,3 +312,68 @@ def test_gp_gemv_handoff_across_calls(rank):
     # the arrival counters (one per 128-B line: n_s (n_cb + 1) of them) lead the workspace and are zero again
     n_ctr = model.n_s * (model._m.C_pad // 128 + 1) * 32
     assert int(model._ws.view(torch.int32)[:n_ctr].abs().sum()) == 0
+
+
+def test_state_from_obs_kernel_matches_reference_get_state(golden):
+    """DynamicsModel.get_state on device fp32 observations is one launch
+    (rcbf_state_from_obs); it returns the reference's own torch get_state
+    output (dynamics.py:190-232, the committed golden) bit for bit, and the
+    torch path on the same rows, for 4 096 random unicycle angles too."""
+    from rcbf_amd.dynamics import DynamicsModel
+    d = golden("dynamics")
+    for nm, mode in (("cars", "SimulatedCars"), ("uni", "Unicycle")):
+        dm = DynamicsModel(types.SimpleNamespace(dynamics_mode=mode, dt=0.02), types.SimpleNamespace(cuda=True))
+        s = dm.get_state(torch.as_tensor(d[nm + "_obs32"], device="cuda"))
+        assert s.dtype == torch.float32 and np.array_equal(s.cpu().numpy(), d[nm + "_state_t"])
+        s1 = dm.get_state(torch.as_tensor(d[nm + "_obs32"][0], device="cuda"))  # 1-D in, 1-D out
+        assert s1.shape == (dm.n_s,) and np.array_equal(s1.cpu().numpy(), d[nm + "_state_t"][0])
+    rng = np.random.default_rng(3)
+    th = rng.uniform(-np.pi, np.pi, 4096)
+    obs = O.uni_obs(np.stack([rng.uniform(-3, 3, 4096), rng.uniform(-3, 3, 4096), th], 1)).astype(np.float32)
+    dm = DynamicsModel(types.SimpleNamespace(dynamics_mode="Unicycle", dt=0.02), types.SimpleNamespace(cuda=True))
+    got = dm.get_state(torch.as_tensor(obs, device="cuda")).cpu().numpy()
+    assert np.array_equal(got, O.get_state_f32("Unicycle", obs))
+
+
+@pytest.mark.parametrize("mode,k", [("SimulatedCars", 0), ("Unicycle", 3)])
+def test_sac_safe_action_with_gp_is_the_reference_three_calls(mode, k):
+    """RCBF_SAC.get_safe_action with a fitted GP (sac_cbf.py:233-236) through
+    rcbf_amd.sac_cbf.get_safe_action -- state kernel, GP kernel, one safe-action
+    launch reading the posterior rows -- equals the reference's three calls on
+    rcbf_amd's surfaces (get_state -> predict_disturbance ->
+    CBFQPLayer.get_safe_action) bit for bit, forward and d final / d action,
+    at B = 1 (the env step) and B = 256 (the SAC update)."""
+    from rcbf_amd import gp
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+    from rcbf_amd.sac_cbf import get_safe_action
+    rng = np.random.default_rng(19 + k)
+    if mode == "SimulatedCars":
+        env = BatchedSimulatedCarsEnv(4)
+        x = np.tile(np.array([34.0, 30, 28, 30, 22, 30, 16, 35, 10, 30]), (1100, 1)) + rng.normal(0, 1.5, (1100, 10))
+    else:
+        env = BatchedUnicycleEnv(4, hazards_locations=O.UNI["hazards"][:k])
+        x = np.stack([rng.uniform(-3, 3, 1100), rng.uniform(-3, 3, 1100), rng.uniform(-np.pi, np.pi, 1100)], 1)
+    n_s = x.shape[1]
+    dm = DynamicsModel(env, types.SimpleNamespace(cuda=True, gp_model_size=1100))
+    hyper = [(1.3, 0.2, 0.05)] * n_s
+    dm.disturb_estimators = gp.GPDisturbanceModel(x, 0.05 * np.sin(x) + rng.normal(0, 0.02, x.shape), hyper,
+                                                  rank=gp.love_rank(1100))
+    layer = CBFQPLayer(env, types.SimpleNamespace(cuda=True), gamma_b=20.0)
+    for B in (1, 256):
+        idx = rng.integers(0, 1100, B)
+        obs = (O.cars_obs(x[idx]) if mode == "SimulatedCars" else O.uni_obs(x[idx])).astype(np.float32)
+        ob = torch.as_tensor(obs, device="cuda")
+        ua = torch.as_tensor(rng.uniform(-1, 1, (B, env.n_u)).astype(np.float32), device="cuda")
+        w = torch.as_tensor(rng.normal(0, 1, (B, env.n_u)).astype(np.float32), device="cuda")
+        u1 = ua.clone().requires_grad_(True)
+        out1 = get_safe_action(layer, ob, u1, dm)
+        (out1 * w).sum().backward()
+        state = dm.get_state(ob)
+        mean, sigma = dm.predict_disturbance(state)
+        u2 = ua.clone().requires_grad_(True)
+        out2 = layer.get_safe_action(state, u2, mean, sigma)
+        (out2 * w).sum().backward()
+        assert torch.equal(out1.detach(), out2.detach()) and torch.equal(u1.grad, u2.grad), B
+        assert bool((out1.detach() != ua).any()) or B == 1  # the filter is active on part of the batch
