@@ -114,6 +114,7 @@ class _Agent:
             with torch.no_grad():
                 a, _, m = self.policy.sample(state)
             action = m if evaluate else a
+        torch.cuda.synchronize()  # the policy's launches are not the safety layer's time
         t0 = time.perf_counter()
         safe = self.get_safe_action(state, action, dynamics_model)
         out = safe.detach().cpu().numpy()
@@ -175,7 +176,7 @@ def _train(env_name, episodes, model_based):
     dm.fit_gp_model = lambda *a, **k: (fits.append(dm.history_counter), fit(*a, **k))
     agent = _Agent(env, args)
     memory, memory_model = ReplayMemory(args.replay_size, args.seed), ReplayMemory(args.replay_size, args.seed)
-    rec = {"steps": 0, "updates": 0, "episodes": [], "step_s": [], "rollout_calls": 0}
+    rec = {"steps": 0, "updates": 0, "episodes": [], "step_s": [], "update_s": [], "rollout_calls": 0}
     lo, hi = env.safe_action_space.low, env.safe_action_space.high
     total = 0
     for _ in range(episodes):
@@ -188,6 +189,7 @@ def _train(env_name, episodes, model_based):
                                                        warmup=args.start_steps > total)
                 rec["rollout_calls"] += 1
             if len(memory) + len(memory_model) * model_based > args.batch_size:
+                t_up = time.perf_counter()
                 for _ in range(args.updates_per_step):
                     if model_based:
                         rr = max(min(args.real_ratio, len(memory) / args.batch_size),
@@ -196,6 +198,8 @@ def _train(env_name, episodes, model_based):
                     else:
                         agent.update_parameters(memory, args.batch_size, rec["updates"], dm)
                     rec["updates"] += 1
+                torch.cuda.synchronize()  # the update's queued tail stays out of the env step's time
+                rec["update_s"].append(time.perf_counter() - t_up)
             t0 = time.perf_counter()
             action = agent.select_action(obs, dm, warmup=args.start_steps > total)
             next_obs, reward, done, info = env.step(action)
@@ -225,13 +229,17 @@ def _record(name, rec):
     out_dir = os.path.join(ROOT, "gpurun_out")
     warm = np.asarray(rec["step_s"][200:]) * 1e6  # past the warm-up actions and first launches
     sa = np.asarray(rec["agent"].safe_action_s[200:]) * 1e6
+    up = np.asarray(rec["update_s"]) * 1e6
     row = {"env_steps": rec["steps"], "updates": rec["updates"], "gp_fits": len(rec["fits"]),
            "rollout_calls": rec["rollout_calls"],
            "env_step_us_median": round(float(np.median(warm)), 1),
            "env_step_us_p90": round(float(np.percentile(warm, 90)), 1),
            "safe_action_us_median": round(float(np.median(sa)), 1),
-           "what": "per env step: select_action (policy MLP + RCBF_SAC.get_safe_action with the GP posterior, "
-                   "B = 1, to numpy) + env.step (rcbf_env_step_sync); safe_action: get_safe_action + .cpu() alone",
+           "update_us_median": round(float(np.median(up)), 1) if up.size else None,
+           "what": "env_step: select_action (policy MLP sample, synchronize, RCBF_SAC.get_safe_action with the GP "
+                   "posterior at B = 1, to numpy) + env.step (rcbf_env_step_sync), after the update's queued work "
+                   "has drained; safe_action: get_safe_action + .cpu() alone; update: update_parameters at "
+                   "B = 256 (two safe-action calls, one with the gradient through the CBF-QP) to its drained end",
            "episodes": rec["episodes"]}
     if os.path.isdir(out_dir):
         path = os.path.join(out_dir, "training_loop_r05.json")
