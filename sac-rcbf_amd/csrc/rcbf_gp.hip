@@ -499,6 +499,7 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
     __shared__ float s_k[BQ][kGvRows];
     __shared__ float4 s_red[4][BQ][32];
     __shared__ float s_bsum[4][BQ];
+    __shared__ float s_half[2][kGpCols];
     __shared__ float s_mean[BQ];
     __shared__ int s_last;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -519,13 +520,15 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
 
     // 1. every load of the tile at once -- this thread's 128 B of Rt, then its training row (t < 64)
     //    and query component (t < BQ D) -- so the whole tile pays one memory round trip.  Rows past
-    //    the tile's end re-read row n0 (in bounds) and get a zero kernel value.
+    //    the tile's end re-read row n0 (in bounds) and get a zero kernel value.  Default-policy loads:
+    //    the factor is re-read by every query until the next refit, and back-to-back calls gain from
+    //    what the caches keep (r05u: B = 1 / 2 / 8 6.29 / 7.30 / 16.4 us with nt, 6.20 / 7.06 / 15.6 without).
     const float* Rp = m.Rt + ((int64_t)i * m.N_pad + n0) * ldc + cb * kGpCols + 4 * (t & 31);
     f32x4 v[RJ];
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
         const int rr = (t >> 5) + 8 * j;
-        v[j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(Rp + (int64_t)(rr < nrows ? rr : 0) * ldc));
+        v[j] = *reinterpret_cast<const f32x4*>(Rp + (int64_t)(rr < nrows ? rr : 0) * ldc);
     }
     const float sl = m.inv_sl[i];
     const float os = m.outscale[i], nz = m.noise[i], ys = m.y_scale[i];
@@ -630,22 +633,37 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
     __syncthreads();
     if (!s_last) return;
     const int r_rank = m.r;
-    // thread t: physical column p = t & 127 of the block, queries b = (t >> 7), (t >> 7) + 2, ...
+    // thread t: physical column p = t & 127 of the block (4-B sc1 loads, a wave instruction reads two whole
+    // lines).  BQ = 1: the workgroup's halves sum the even and the odd tiles, added in that order through LDS;
+    // a tile's half depends on its index alone, so the exact-zero tiles a dense pass adds past an upper
+    // factor's block change no sum.  BQ > 1: half t >> 7 takes queries b = (t >> 7), (t >> 7) + 2, ...
     const int p = t & 127;
     const int lc = cb * kGpCols + 32 * (p & 3) + (p >> 2);  // logical column (4 l + c holds 32 c + l)
     float vq[(BQ + 1) / 2];
-#pragma unroll
-    for (int h = 0; h < (BQ + 1) / 2; ++h) {
-        const int b = (t >> 7) + 2 * h;
-        float q = 0.0f;
-        if (b < BQ) {
-            q = sum_sc1(part + (((int64_t)i * T + base) * BQ + b) * kGpCols + p, nrc, (int64_t)BQ * kGpCols);
-            if (lc == r_rank && b < B) {
-                st_sc1(meanraw + (int64_t)i * BQ + b, q);
-                s_mean[b] = q;
-            }
+    if constexpr (BQ == 1) {
+        const int g = t >> 7, ng = (nrc - g + 1) / 2;
+        s_half[g][p] = ng > 0 ? sum_sc1(part + ((int64_t)i * T + base + g) * kGpCols + p, ng, 2 * kGpCols) : 0.0f;
+        __syncthreads();
+        const float q = s_half[0][p] + s_half[1][p];
+        if (t < kGpCols && lc == r_rank) {
+            st_sc1(meanraw + (int64_t)i * BQ, q);
+            s_mean[0] = q;
         }
-        vq[h] = (lc < r_rank) ? q * q : 0.0f;
+        vq[0] = (t < kGpCols && lc < r_rank) ? q * q : 0.0f;
+    } else {
+#pragma unroll
+        for (int h = 0; h < (BQ + 1) / 2; ++h) {
+            const int b = (t >> 7) + 2 * h;
+            float q = 0.0f;
+            if (b < BQ) {
+                q = sum_sc1(part + (((int64_t)i * T + base) * BQ + b) * kGpCols + p, nrc, (int64_t)BQ * kGpCols);
+                if (lc == r_rank && b < B) {
+                    st_sc1(meanraw + (int64_t)i * BQ + b, q);
+                    s_mean[b] = q;
+                }
+            }
+            vq[h] = (lc < r_rank) ? q * q : 0.0f;
+        }
     }
 #pragma unroll
     for (int h = 0; h < (BQ + 1) / 2; ++h) {

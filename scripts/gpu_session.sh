@@ -124,8 +124,9 @@ for step in "$@"; do
     gpt)    run gpt 600 python -u -m pytest tests/test_gpu_gp.py tests/test_gpu_parity.py -q -rf --timeout 300 --timeout-method thread ;;
     loop)   run loop 900 python -u -m pytest tests/test_gpu_training_loop.py -q -rf -s --timeout 600 --timeout-method thread ;;
     gpgb)   run gpgb 300 python -u scripts/gp_graph_bench.py ;;
+    single) run single 300 python -u scripts/single_env_latency.py ;;
     gvstudy)  # GEMV study variants (build/variants/librcbf_gv*.so) vs the product, GP graph bench
-      for n in prod gv1 gv3 gvr128; do
+      for n in prod ${GV_VARIANTS:-gv1 gv3 gvr128}; do
         if [ "$n" = prod ]; then lib=""; else lib="RCBF_HIP_LIB=build/variants/librcbf_$n.so"; fi
         env $lib timeout -k 10 200 python scripts/gp_graph_bench.py > "$OUT/gvstudy_$n.log" 2>&1 || exit 1
       done ;;

@@ -1,8 +1,11 @@
 """Per-call host latency of the B = 1 drop-in surfaces the reference's
 training loop calls every env step (main.py:93-110): the gym env.step on a
 numpy action, CBFQPLayer.get_safe_action on 1-D device tensors, and
-RCBF_SAC.get_safe_action (rcbf_amd.sac_cbf) on one observation.  Prints one
-JSON line of microseconds per call (median of 5 runs of 200 calls)."""
+RCBF_SAC.get_safe_action (rcbf_amd.sac_cbf) on one observation, without and
+with a fitted GP (300 points, Lanczos rank 16, the training-loop test's
+setting): back to back, and as select_action takes it (each call followed by
+.cpu(), i.e. one host round trip), with its three launches timed apart.
+Prints one JSON line of microseconds per call (median of 5 runs of 200 calls)."""
 import json
 import os
 import sys
@@ -14,6 +17,20 @@ for p in (ROOT, os.path.join(ROOT, "sac-rcbf_amd")):
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
+
+
+def gp_dynamics(env, rng):
+    """A DynamicsModel with its GP fitted on 300 transitions around the prior."""
+    import types
+    from rcbf_amd.dynamics import DynamicsModel
+    dm = DynamicsModel(env, types.SimpleNamespace(cuda=True, gp_model_size=300, gp_rank=16))
+    n_u = env.action_space.shape[0]
+    x = rng.uniform(-1, 1, (300, dm.n_s)) * (30.0 if dm.n_s == 10 else 3.0)
+    u = rng.uniform(-1, 1, (300, n_u))
+    nx = x + 0.02 * (np.sin(x) + rng.normal(0, 0.05, x.shape))
+    dm.append_transition(x, u, nx, t_batch=rng.uniform(0, 15, 300))
+    assert dm.disturb_estimators is not None
+    return dm
 
 
 def per_call_us(fn, n=200, reps=5):
@@ -61,6 +78,16 @@ def main():
         out[f"{name}_layer_safe_action_us"] = per_call_us(lambda: layer.get_safe_action(st, u, mu, sg))
         ot = torch.as_tensor(obs, dtype=torch.float32, device="cuda")
         out[f"{name}_sac_get_safe_action_us"] = per_call_us(lambda: get_safe_action(layer, ot, u, dm))
+        gdm = gp_dynamics(env, rng)
+        gpm = gdm.disturb_estimators
+        o2 = ot.unsqueeze(0)
+        s2 = gdm.get_state(o2)
+        out[f"{name}_gp_sac_get_safe_action_us"] = per_call_us(lambda: get_safe_action(layer, ot, u, gdm))
+        out[f"{name}_gp_sac_get_safe_action_to_host_us"] = per_call_us(
+            lambda: get_safe_action(layer, ot, u, gdm).cpu())
+        out[f"{name}_gp_get_state_us"] = per_call_us(lambda: gdm.get_state(o2))
+        out[f"{name}_gp_predict_us"] = per_call_us(lambda: gpm.predict(s2))
+        out[f"{name}_to_host_us"] = per_call_us(lambda: u.cpu())
     print(json.dumps(out), flush=True)
 
 
