@@ -71,6 +71,9 @@ def parse():
                     help="prior: the DynamicsModel prior in-kernel (before any GP fit); tensor: per-env mean/sigma "
                          "read from HBM (after the GP fit) in the column layout the GP writes for the step "
                          "(rcbf_gp_predict_cols -> rcbf_safe_step_cols); rows: the same as (B, n_s) row tensors")
+    ap.add_argument("--rccl", action="store_true",
+                    help="bring up the RCCL process group even on one rank: the N > 1 path's init, barriers, "
+                         "all_gather and MAX all_reduce then run on the device (world size 1)")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="CPU/gloo plumbing check of the launcher (no kernel, no measurement)")
     ap.add_argument("--launch", default="graph", choices=["graph", "seq"],
@@ -286,6 +289,14 @@ def init_states(env, gen, env_name):
     torch.cuda.synchronize()
 
 
+def free_port():
+    """A free TCP port on the loopback address (the rendezvous of spawned or single ranks)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
 def spawn_ranks(n):
     """`bench.py --gpus N` run as a plain process: start N rank processes of
     this same script BEFORE anything touches the GPU (this parent never
@@ -293,11 +304,8 @@ def spawn_ranks(n):
     LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT).  Rank
     0 inherits stdout and prints the JSON line.  If a rank fails the others
     are stopped; returns the first non-zero exit status (0 if all succeed)."""
-    import socket
     import subprocess
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
+    port = free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
@@ -545,7 +553,12 @@ def main():
             raise SystemExit(f"rank {rank}: LOCAL_RANK {local}, but {torch.cuda.device_count()} HIP device(s) visible")
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        if world > 1:
+        if world > 1 or args.rccl:
+            if world == 1:  # one rank: a rendezvous of its own on the loopback address
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", str(free_port()))
+                os.environ.setdefault("RANK", "0")
+                os.environ.setdefault("WORLD_SIZE", "1")
             dist.init_process_group("nccl", device_id=dev)
         setup = setup_sac_update if args.workload == "sac_update" else setup_gpu
         env, layer, graph, S, active_frac, untimed, ctx = setup(args, dev, rank, B)
@@ -575,8 +588,11 @@ def main():
     if not args.cpu_dry_run:
         ev1.record()
     sync()
-    shard.barrier(world)
+    # this rank's K steps end at its own synchronize; the closing barrier only brackets the region (an RCCL
+    # barrier is a device collective of tens of us, r05y: 20 steps 5.3 -> 7.7 us per step with it inside)
+    # and the MAX over ranks below makes the slowest rank's time the job's
     el = time.perf_counter() - t0
+    shard.barrier(world)
     # per fused-step launch, HIP events on the launch stream (torch's current stream)
     kern_ms = ev0.elapsed_time(ev1) / args.steps if not args.cpu_dry_run else 0.0
     env.check_failures()
@@ -634,6 +650,9 @@ def main():
                    "baseline_config": args.config or None,
                    "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
                    "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)",
+                   "collectives": (f"RCCL process group, world {world}: barrier around the timed region, "
+                                   "all_gather of per-rank times, MAX all_reduce of the per-launch time"
+                                   if dist.is_available() and dist.is_initialized() else None),
                    "prior": args.prior, "qp_active_frac_at_start": round(active_frac, 4),
                    "host_cores_per_rank": len(host_cores) if host_cores else None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -677,7 +696,7 @@ def main():
         rec.update(cpu_baselines_in_child(args))
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -28,14 +28,19 @@ def env_offset(rank, per_rank):
     return rank * per_rank
 
 
+def _group_on():
+    """A process group is up (world > 1, or bench.py --rccl on one rank)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def barrier(world):
-    if world > 1:
+    if world > 1 or _group_on():
         dist.barrier()
 
 
 def max_over_ranks(x, world, device):
     """The slowest rank's value (elapsed time, per-launch time)."""
-    if world <= 1:
+    if world <= 1 and not _group_on():
         return float(x)
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -51,7 +56,7 @@ def whole_job_rate(world, per_rank, steps, elapsed_max):
 def gather_over_ranks(x, world, device):
     """Every rank's value, in rank order (for the per-rank spread of the
     timed region in bench.py's N > 1 line)."""
-    if world <= 1:
+    if world <= 1 and not _group_on():
         return [float(x)]
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     out = [torch.zeros_like(t) for _ in range(world)]
