@@ -275,9 +275,11 @@ def test_gp_gemv_handoff_across_calls(rank):
     """The one-launch GEMV (B <= 8) hands its tile partials to the last
     arriving workgroup through write-through stores and arrival counters that
     the consumers reset: 48 back-to-back calls on one workspace, each with
-    its own queries (B cycling 1, 2, 3, 8), captured in one hipGraph, every
-    output against the oracle -- a stale partial or a counter left non-zero
-    would reuse an earlier call's values.  The counters are zero afterwards."""
+    its own queries (B cycling 1, 2, 3, 8), captured in one hipGraph and
+    replayed three times (the third beside GEMMs on another stream, so the
+    workgroups arrive unevenly), every output against the oracle -- a stale
+    partial or a counter left non-zero would reuse an earlier call's values.
+    The counters are zero afterwards."""
     from rcbf_amd import gp
     rng = np.random.default_rng(77 + (rank or 0))
     tx, ty = _data(rng, 1500, 10)
@@ -301,10 +303,17 @@ def test_gp_gemv_handoff_across_calls(rank):
                                      _lib.ptr(outs[j][1]), _lib.ptr(model._ws), _lib.stream_of(torch.device("cuda")))
             assert rc == 0
     mo, so = O.gp_predict(q, tx, ty, hyper, rank=rank, love_init=None if rank is None else model.love_init.numpy())
-    for _ in range(2):
+    side = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device="cuda")
+    for rep in range(3):
         for o in outs:
             o[0].zero_()
             o[1].zero_()
+        torch.cuda.synchronize()
+        if rep == 2:  # uneven load (G16): GEMMs on a second stream hold CUs while the 48 calls run
+            with torch.cuda.stream(side):
+                for _ in range(6):
+                    a = (a @ a).clamp_(-1, 1)
         g.replay()
         torch.cuda.synchronize()
         for j in range(48):
