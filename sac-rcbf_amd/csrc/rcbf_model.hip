@@ -15,6 +15,71 @@ using namespace rcbf;
 
 namespace {
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// The workgroup's rows (W elements of T each, row-major, rows row0 .. row0 + nrows) through LDS, so the
+// global accesses are whole coalesced 16-B lane vectors; a row per lane would put the lanes W sizeof(T)
+// bytes apart, each of its W load instructions touching a line per 1-2 lanes.  16-B accesses when the block's first element is 16-B aligned (a tensor's own storage is;
+// a sliced view may not be), element accesses otherwise; all of a thread's loads are issued before its
+// LDS stores.  s: kBlock * W elements, 16-B aligned.
+template <typename T, int W>
+__device__ __forceinline__ void rows_in(const T* __restrict__ src, int64_t row0, int nrows, T* s) {
+    constexpr int V = 16 / (int)sizeof(T);
+    const T* p = src + row0 * W;
+    const int n = nrows * W, t = threadIdx.x;
+    if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+        constexpr int kIt = (kBlock * W / V + kBlock - 1) / kBlock;
+        const int nv = n / V;
+        u32x4 v[kIt];
+#pragma unroll
+        for (int j = 0; j < kIt; ++j) {
+            const int e = t + j * kBlock;
+            if (e < nv) v[j] = reinterpret_cast<const u32x4*>(p)[e];
+        }
+#pragma unroll
+        for (int j = 0; j < kIt; ++j) {
+            const int e = t + j * kBlock;
+            if (e < nv) reinterpret_cast<u32x4*>(s)[e] = v[j];
+        }
+        if (t < n - nv * V) s[nv * V + t] = p[nv * V + t];
+    } else {
+        T v[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            const int e = t + j * kBlock;
+            if (e < n) v[j] = p[e];
+        }
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            const int e = t + j * kBlock;
+            if (e < n) s[e] = v[j];
+        }
+    }
+}
+
+template <typename T, int W>
+__device__ __forceinline__ void rows_out(T* __restrict__ dst, int64_t row0, int nrows, const T* s) {
+    constexpr int V = 16 / (int)sizeof(T);
+    T* p = dst + row0 * W;
+    const int n = nrows * W, t = threadIdx.x;
+    if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+        constexpr int kIt = (kBlock * W / V + kBlock - 1) / kBlock;
+        const int nv = n / V;
+#pragma unroll
+        for (int j = 0; j < kIt; ++j) {
+            const int e = t + j * kBlock;
+            if (e < nv) reinterpret_cast<u32x4*>(p)[e] = reinterpret_cast<const u32x4*>(s)[e];
+        }
+        if (t < n - nv * V) p[nv * V + t] = s[nv * V + t];
+    } else {
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            const int e = t + j * kBlock;
+            if (e < n) p[e] = s[e];
+        }
+    }
+}
+
 // get_state (dynamics.py:190-232), numpy fp64 path
 template <int MODE>
 __device__ __forceinline__ void model_state_from_obs(const double* o, double* xs) {
@@ -175,29 +240,61 @@ __global__ void __launch_bounds__(kBlock) k_predict_next_state(int64_t B, const 
 #pragma clang fp contract(off)
     using D = Dims<MODE, 1>;
     constexpr int NS = D::NS, NU = D::NU;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= B) return;
+    // the cars' 80-B rows (x in; next_x, std_out out; 40-B mean / std in) go through LDS (rows_in /
+    // rows_out): 11.1 -> 8.0 us at B = 65 536 (r05zb); the unicycle's 24-B rows stay per lane (3.8 us
+    // per lane, 4.0 staged), as do the model step's rows (6.2 us per lane, 6.4 staged: its time is the
+    // fp64 sin / Philox chain, not the access pattern)
+    constexpr bool kStage = NS * (int)sizeof(double) >= 64;
+    constexpr int kS = kStage ? kBlock * NS / 2 + 1 : 1, kM = kStage ? kBlock * NS / 4 + 1 : 1;
+    __shared__ u32x4 s_x[kS], s_sd[kS], s_ms[2][kM];
+    double* sx = reinterpret_cast<double*>(s_x);
+    double* sd_rows = reinterpret_cast<double*>(s_sd);
+    const int64_t row0 = (int64_t)blockIdx.x * kBlock;
+    const int nrows = (int)min((int64_t)kBlock, B - row0);
+    const int64_t i = row0 + threadIdx.x;
+    const bool live = threadIdx.x < nrows;
+    if constexpr (!kStage) {
+        if (!live) return;
+    } else {
+        rows_in<double, NS>(x, row0, nrows, sx);
+        if (use_gps && mean) rows_in<float, NS>(mean, row0, nrows, reinterpret_cast<float*>(s_ms[0]));
+        if (use_gps && stdv) rows_in<float, NS>(stdv, row0, nrows, reinterpret_cast<float*>(s_ms[1]));
+    }
     const double dt = 0.02;
     double xs[NS], u[NU], nx[NS];
 #pragma unroll
-    for (int k = 0; k < NS; ++k) xs[k] = x[i * NS + k];
+    for (int c = 0; c < NU; ++c) u[c] = live ? act[i * NU + c] : 0.0;
+    const double ti = (t && live) ? t[i] : 0.0;
+    if constexpr (kStage) __syncthreads();
 #pragma unroll
-    for (int c = 0; c < NU; ++c) u[c] = act[i * NU + c];
-    const double ti = t ? t[i] : 0.0;
+    for (int k = 0; k < NS; ++k) xs[k] = kStage ? sx[threadIdx.x * NS + k] : x[i * NS + k];
     model_prior_next<MODE>(xs, u, ti, nx);
+    const float* sm = kStage ? reinterpret_cast<const float*>(s_ms[0]) + threadIdx.x * NS : mean + i * NS;
+    const float* ss = kStage ? reinterpret_cast<const float*>(s_ms[1]) + threadIdx.x * NS : stdv + i * NS;
+    if constexpr (kStage) __syncthreads();  // every thread has read its x row: the buffer takes the next_x rows
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
         double sd = 0.0;
         if (use_gps) {
-            const double m = mean ? (double)mean[i * NS + k] : 0.0;
+            const double m = mean ? (double)sm[k] : 0.0;
             const double prior = (MODE == RCBF_MODE_UNICYCLE || (k & 1)) ? 0.2 : 0.0;  // MAX_STD
-            sd = stdv ? (double)stdv[i * NS + k] : prior;
+            sd = stdv ? (double)ss[k] : prior;
             nx[k] = nx[k] + dt * m;  // next_state_batch += dt * pred_mean
         }
-        next_x[i * NS + k] = nx[k];
-        std_out[i * NS + k] = dt * sd;
+        if constexpr (kStage) {
+            sx[threadIdx.x * NS + k] = nx[k];
+            sd_rows[threadIdx.x * NS + k] = dt * sd;
+        } else {
+            next_x[i * NS + k] = nx[k];
+            std_out[i * NS + k] = dt * sd;
+        }
     }
-    if (next_t) next_t[i] = ti + dt;
+    if (next_t && live) next_t[i] = ti + dt;
+    if constexpr (kStage) {
+        __syncthreads();
+        rows_out<double, NS>(next_x, row0, nrows, sx);
+        rows_out<double, NS>(std_out, row0, nrows, sd_rows);
+    }
 }
 
 // Replay ring (rcbf_sac/replay_memory.py:12-32): records are rows of W f64.

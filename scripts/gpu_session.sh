@@ -125,6 +125,13 @@ for step in "$@"; do
     loop)   run loop 900 python -u -m pytest tests/test_gpu_training_loop.py -q -rf -s --timeout 600 --timeout-method thread ;;
     gpgb)   run gpgb 300 python -u scripts/gp_graph_bench.py ;;
     single) run single 300 python -u scripts/single_env_latency.py ;;
+    msab)   # model step / predict_next_state: product vs build/variants/librcbf_modelold.so, 3 rounds
+      for r in 1 2 3; do for n in prod modelold; do
+        if [ "$n" = prod ]; then lib=""; else lib="RCBF_HIP_LIB=build/variants/librcbf_$n.so"; fi
+        env $lib timeout -k 10 200 python scripts/model_step_bench.py > "$OUT/ms_${n}_$r.log" 2>&1 || exit 1
+        echo "$n $(tail -1 "$OUT/ms_${n}_$r.log")" >> "$OUT/msab_sum.txt"
+      done; done ;;
+    gpm)    run gpm 300 python -u -m pytest tests/test_gpu_model.py -q -rf --timeout 200 --timeout-method thread ;;
     rccl)   run rccl 300 python bench.py --rccl --steps 20 --warmup 5 --no-cpu-baseline ;;  # the N > 1 collectives on one rank
     gvstudy)  # GEMV study variants (build/variants/librcbf_gv*.so) vs the product, GP graph bench
       for n in prod ${GV_VARIANTS:-gv1 gv3 gvr128}; do

@@ -28,7 +28,8 @@ def _check(m, s, mo, so):
 
 
 @pytest.mark.parametrize("n_s,N,B", [(3, 300, 1), (3, 1100, 4096), (10, 1000, 200), (10, 3000, 257),
-                                     (10, 3000, 1), (10, 1000, 5), (3, 300, 8), (3, 1100, 2)])
+                                     (10, 3000, 1), (10, 1000, 5), (3, 300, 8), (3, 1100, 2),
+                                     (3, 40, 1), (10, 64, 1), (3, 33, 8), (10, 65, 1)])
 def test_gp_predict_vs_oracle(n_s, N, B):
     from rcbf_amd import gp
     rng = np.random.default_rng(n_s * N + B)
