@@ -1045,7 +1045,8 @@ def _qp_pair_times(lib, prm_struct, P, q, G, h, gen, dev):
 
 
 def _time_graph(fn, reps, dev):
-    """Mean ms per fn() call, fn captured `reps` times in one hipGraph."""
+    """Mean ms per fn() call, fn captured `reps` times in one hipGraph, the best of 3 replays (each
+    replay's events also hold the graph's start, ~15 us: keep reps * per-call time well above it)."""
     s = torch.cuda.Stream(device=dev)
     with torch.cuda.stream(s):
         fn()
@@ -1057,11 +1058,15 @@ def _time_graph(fn, reps, dev):
     g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    g.replay()
-    e1.record()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps
+    best = None
+    for _ in range(3):
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        best = ms if best is None else min(best, ms)
+    return best
 
 
 def next_rows(dev):
@@ -1082,13 +1087,13 @@ def next_rows(dev):
     model = gp.GPDisturbanceModel(tx, ty, [(1.5, 0.2, 0.05)] * 10, device=dev)
     for B in (1, 256, 4096):
         x = torch.as_tensor(rng.normal(0, 1, (B, 10)), dtype=torch.float32, device=dev)
-        ms = _time_graph(lambda: model.predict(x), 5, dev)
+        ms = _time_graph(lambda: model.predict(x), 20 if B <= 256 else 5, dev)
         out[f"gp_predict_N3000_B{B}"] = {"ms": round(ms, 4), "tflops": round(model.flops_per_query() * B / ms / 1e9, 1),
                                           "frac_fp32_mfma_157TF": round(model.flops_per_query() * B / ms / 1e9 / 157.3, 3)}
     lr = gp.GPDisturbanceModel(tx, ty, [(1.5, 0.2, 0.05)] * 10, device=dev, rank=100)
     for B in (1, 256, 4096):  # rank 100: the root-decomposition size of gpytorch's fast_pred_var
         x = torch.as_tensor(rng.normal(0, 1, (B, 10)), dtype=torch.float32, device=dev)
-        ms = _time_graph(lambda: lr.predict(x), 5, dev)
+        ms = _time_graph(lambda: lr.predict(x), 20 if B <= 256 else 5, dev)
         out[f"gp_predict_N3000_rank100_B{B}"] = {"us": round(ms * 1e3, 2),
                                                   "tflops": round(lr.flops_per_query() * B / ms / 1e9, 2)}
     B = 65536
@@ -1106,6 +1111,14 @@ def next_rows(dev):
     ms = _time_graph(step, 20, dev)
     out["model_step_cars_B65536"] = {"us": round(ms * 1e3, 2), "rows_per_s": round(B / ms * 1e3, 1),
                                      "GBs": round(B * 200 / ms / 1e6, 1)}
+    # DynamicsModel.predict_next_state on device rows with the GP mean / std (f32): x, act, t, mean, std in;
+    # next_x, std_out, next_t out = 80 + 8 + 8 + 40 + 40 + 80 + 80 + 8 = 344 B per row
+    mean, std = (torch.rand(B, 10, dtype=torch.float32, device=dev) for _ in range(2))
+    nx, so = torch.empty_like(obs), torch.empty_like(obs)
+    ms = _time_graph(lambda: lib.rcbf_predict_next_state(ctypes.byref(prm), B, _lib.ptr(obs), _lib.ptr(act),
+                                                         _lib.ptr(t), _lib.ptr(mean), _lib.ptr(std), 1, _lib.ptr(nx),
+                                                         _lib.ptr(so), _lib.ptr(nt), _lib.stream_of(dev)), 20, dev)
+    out["predict_next_state_gp_cars_B65536"] = {"us": round(ms * 1e3, 2), "GBs": round(B * 344 / ms / 1e6, 1)}
     W, cap = 25, 1 << 20
     ring = torch.zeros(cap, W, dtype=torch.float64, device=dev)
     src = torch.rand(B, W, dtype=torch.float64, device=dev)
