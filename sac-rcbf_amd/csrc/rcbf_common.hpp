@@ -24,8 +24,20 @@ inline unsigned grid_for(int64_t B) { return (unsigned)((B + kBlock - 1) / kBloc
 inline unsigned grid_for_envs(int64_t B) { return grid_for(B); }
 
 // env index of this lane in the env kernels: one env per lane
+#ifndef RCBF_STUDY_EPW
 template <int BS = kBlock>
 __device__ __forceinline__ int64_t env_index() { return (int64_t)blockIdx.x * BS + threadIdx.x; }
+#else
+// study build (scripts/epw_study.sh): the one-wave (64-thread) workgroups of small batches carry only
+// RCBF_STUDY_EPW envs, on lanes 0 .. EPW - 1 (the rest exit: their index is past any B), so a batch
+// reaches 64 / EPW times as many CUs
+template <int BS = kBlock>
+__device__ __forceinline__ int64_t env_index() {
+    if constexpr (BS == 64)
+        return threadIdx.x < RCBF_STUDY_EPW ? (int64_t)blockIdx.x * RCBF_STUDY_EPW + threadIdx.x : INT64_MAX;
+    return (int64_t)blockIdx.x * BS + threadIdx.x;
+}
+#endif
 
 // Workgroup size of the fused step for a batch of B envs.  The step is a
 // per-CU memory-request-bound chain at one wave per SIMD (half
@@ -56,7 +68,14 @@ inline int block_for_envs(int64_t B) {
 #else
 inline int block_for_envs(int64_t) { return 256; }
 #endif
+#ifndef RCBF_STUDY_EPW
 inline unsigned grid_for_envs(int64_t B, int bs) { return (unsigned)((B + bs - 1) / bs); }
+#else
+inline unsigned grid_for_envs(int64_t B, int bs) {
+    const int e = bs == 64 ? RCBF_STUDY_EPW : bs;
+    return (unsigned)((B + e - 1) / e);
+}
+#endif
 
 // Memory policy of the env kernels: every once-read input is an `nt` load and
 // every output an `nt` store (with the whole-line stores below the fastest of

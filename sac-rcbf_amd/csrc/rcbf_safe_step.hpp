@@ -125,7 +125,11 @@ __device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_
     constexpr int NO = Dims<MODE, 1>::NO;
     const int lane = threadIdx.x & 63;
     const int64_t base = i - lane;
+#ifdef RCBF_STUDY_EPW  // study: a 64-thread workgroup's wave holds fewer than 64 envs (per-lane stores)
+    const bool full = blockDim.x != 64 && (base + 64 <= B) && ((reinterpret_cast<uintptr_t>(obs) & 15) == 0);
+#else
     const bool full = (base + 64 <= B) && ((reinterpret_cast<uintptr_t>(obs) & 15) == 0);
+#endif
     if (!full) {
         store_obs32<MODE>(obs, i, xs, obs_cache);
         return;

@@ -131,6 +131,13 @@ for step in "$@"; do
         env $lib timeout -k 10 200 python scripts/model_step_bench.py > "$OUT/ms_${n}_$r.log" 2>&1 || exit 1
         echo "$n $(tail -1 "$OUT/ms_${n}_$r.log")" >> "$OUT/msab_sum.txt"
       done; done ;;
+    epw)    # lanes-per-wave study for small batches (build/variants/librcbf_epw{16,32}.so): parity, then A/B
+      for n in epw16 epw32; do
+        RCBF_HIP_LIB=build/variants/librcbf_$n.so run "epw_parity_$n" 300 python -u -m pytest tests/test_gpu_headline_parity.py \
+          -q -rf -k "small_batch or config4_eight" --timeout 200 --timeout-method thread
+        grep -q " passed" "$OUT/epw_parity_$n.log" || exit 1
+      done
+      bash scripts/ab_multi.sh "$TAG/epwab" "epw16 epw32" c2 c3 c5 || exit 1 ;;
     gpm)    run gpm 300 python -u -m pytest tests/test_gpu_model.py -q -rf --timeout 200 --timeout-method thread ;;
     rccl)   run rccl 300 python bench.py --rccl --steps 20 --warmup 5 --no-cpu-baseline ;;  # the N > 1 collectives on one rank
     gvstudy)  # GEMV study variants (build/variants/librcbf_gv*.so) vs the product, GP graph bench
