@@ -1,7 +1,7 @@
 """One GP posterior batch size, for counter passes (rocprofv3 --pmc) and
 A/B timing: N = 3000 training points, n_s GPs, exact variance, B queries,
 `reps` predictions after two warm-up calls; prints ms per prediction (HIP
-events on the launch stream).
+events on the launch stream).  GP_RANK=r: LOVE's rank-r Lanczos factor instead.
 Usage: python scripts/gp_one.py B [reps] [n_s] [N]"""
 import os
 import sys
@@ -20,7 +20,8 @@ N = int(sys.argv[4]) if len(sys.argv) > 4 else 3000
 rng = np.random.default_rng(0)
 tx = rng.normal(0, 1, (N, n_s))
 ty = 0.1 * np.sin(tx) + rng.normal(0, 0.05, (N, n_s))
-model = gp.GPDisturbanceModel(tx, ty, [(1.5, 0.2, 0.05)] * n_s)
+rank = int(os.environ["GP_RANK"]) if os.environ.get("GP_RANK") else None  # e.g. 100: LOVE's Lanczos factor
+model = gp.GPDisturbanceModel(tx, ty, [(1.5, 0.2, 0.05)] * n_s, rank=rank)
 if os.environ.get("RCBF_GP_DENSE"):  # A/B: read the whole [R | alpha] (no upper-triangular skip)
     model._m.flags = 0
 x = torch.as_tensor(rng.normal(0, 1, (B, n_s)), dtype=torch.float32, device="cuda")

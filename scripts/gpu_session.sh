@@ -138,6 +138,14 @@ for step in "$@"; do
         grep -q " passed" "$OUT/epw_parity_$n.log" || exit 1
       done
       bash scripts/ab_multi.sh "$TAG/epwab" "epw16 epw32" c2 c3 c5 || exit 1 ;;
+    gppmc)  # HBM traffic of the rank-100 GEMV at B = 1 (eager calls; FETCH_SIZE and WRITE_SIZE in their own passes)
+      GP_RANK=100 run gppmc_f 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/gppmc_f" -o run -- python3 scripts/gp_one.py 1 50
+      GP_RANK=100 run gppmc_w 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/gppmc_w" -o run -- python3 scripts/gp_one.py 1 50
+      if [ -f "$OUT/gppmc_f/run_counter_collection.csv" ] && [ -f "$OUT/gppmc_w/run_counter_collection.csv" ]; then
+        python scripts/pmc_traffic.py "$OUT/gppmc_f/run_counter_collection.csv" "$OUT/gppmc_w/run_counter_collection.csv" \
+          "k_gp_gemv<10, 1>" "$OUT/pmc_traffic_gp_gemv_rank100_B1.json" workload="GP N=3000 rank 100 B=1" \
+          algorithmic_read_bytes=16724480 > /dev/null
+      fi ;;
     gpm)    run gpm 300 python -u -m pytest tests/test_gpu_model.py -q -rf --timeout 200 --timeout-method thread ;;
     rccl)   run rccl 300 python bench.py --rccl --steps 20 --warmup 5 --no-cpu-baseline ;;  # the N > 1 collectives on one rank
     gvstudy)  # GEMV study variants (build/variants/librcbf_gv*.so) vs the product, GP graph bench
