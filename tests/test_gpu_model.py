@@ -229,3 +229,44 @@ def test_predict_next_state_device_edge_cases():
         dm.predict_next_state(x, u, t_batch=None, use_gps=False)
     nx, sd, nt = dm.predict_next_state(x[:0], u[:0], t_batch=torch.zeros(0, dtype=torch.float64, device="cuda"))
     assert nx.shape == (0, 10) and sd.shape == (0, 10) and nt.shape == (0,)
+
+
+def test_predict_next_state_staged_rows_ragged_and_unaligned():
+    """The cars kernel stages its 80-B rows through LDS (16-B accesses when
+    the block's rows start 16-B aligned, element accesses otherwise): a
+    ragged batch (B = 777: three full workgroups and a partial one) from an
+    aligned buffer and from a view 8 bytes into one (the unaligned path)
+    gives the same values bit for bit, the numpy path's within the device
+    fp64 sin's ulps (car 0's v_des = 30 - 10 sin(0.2 t); random t here, the
+    golden rows of test_predict_next_state_device_vs_reference are
+    bit-exact), with the GP mean / std rows too."""
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.envs import SimulatedCarsEnv
+    dm = DynamicsModel(SimulatedCarsEnv(), types.SimpleNamespace(cuda=True))
+    rng = np.random.default_rng(5)
+    B = 777
+    st = np.tile(np.array([34.0, 30.0, 28.0, 30.0, 22.0, 30.0, 16.0, 35.0, 10.0, 30.0]), (B, 1)) + rng.normal(0, 1, (B, 10))
+    u = rng.uniform(-1, 1, (B, 1))
+    t = np.round(rng.uniform(0, 6, B) / 0.02) * 0.02
+    ref_nx, ref_sd, _ = dm.predict_next_state(st, u, t_batch=t, use_gps=False)
+    ud, td = torch.as_tensor(u, device="cuda"), torch.as_tensor(t, device="cuda")
+    buf = torch.zeros(B * 10 + 1, dtype=torch.float64, device="cuda")
+    outs = []
+    for x in (torch.as_tensor(st, device="cuda"), buf[1:].view(B, 10)):
+        x.copy_(torch.as_tensor(st, device="cuda"))
+        assert (x.data_ptr() % 16 == 0) == (x.storage_offset() == 0)
+        nx, sd, nt = dm.predict_next_state(x, ud, t_batch=td, use_gps=False)
+        assert np.max(np.abs(nx.cpu().numpy() - ref_nx)) <= 1e-13 * np.max(np.abs(ref_nx))
+        assert not sd.cpu().numpy().any() and np.array_equal(nt.cpu().numpy(), t + 0.02)
+        outs.append(nx.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    m32 = rng.normal(0, 0.05, (B, 10)).astype(np.float32)
+    s32 = rng.uniform(0.01, 0.3, (B, 10)).astype(np.float32)
+
+    class _GP:
+        def predict(self, xq):
+            return torch.as_tensor(m32, device=xq.device), torch.as_tensor(s32, device=xq.device)
+    dm.disturb_estimators = _GP()
+    nx, sd, _ = dm.predict_next_state(buf[1:].view(B, 10), ud, t_batch=td, use_gps=True)
+    assert np.array_equal(nx.cpu().numpy(), outs[0] + 0.02 * m32.astype(np.float64))
+    assert np.array_equal(sd.cpu().numpy(), 0.02 * s32.astype(np.float64))
