@@ -289,6 +289,15 @@ def init_states(env, gen, env_name):
     torch.cuda.synchronize()
 
 
+def one_rank_rendezvous(world):
+    """--rccl on one rank: a rendezvous of its own on the loopback address."""
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+
+
 def free_port():
     """A free TCP port on the loopback address (the rendezvous of spawned or single ranks)."""
     import socket
@@ -541,7 +550,8 @@ def main():
     host_mask = host_cores = None
     if args.cpu_dry_run:
         dev = torch.device("cpu")
-        if world > 1:
+        if world > 1 or args.rccl:  # --rccl on one rank: the same group code, over gloo
+            one_rank_rendezvous(world)
             dist.init_process_group("gloo")
         S, reps = args.steps, 1
         graph = env = _DryRun(B, 1 if args.env == "SimulatedCars" else 2)
@@ -554,11 +564,7 @@ def main():
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         if world > 1 or args.rccl:
-            if world == 1:  # one rank: a rendezvous of its own on the loopback address
-                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-                os.environ.setdefault("MASTER_PORT", str(free_port()))
-                os.environ.setdefault("RANK", "0")
-                os.environ.setdefault("WORLD_SIZE", "1")
+            one_rank_rendezvous(world)
             dist.init_process_group("nccl", device_id=dev)
         setup = setup_sac_update if args.workload == "sac_update" else setup_gpu
         env, layer, graph, S, active_frac, untimed, ctx = setup(args, dev, rank, B)
@@ -650,7 +656,8 @@ def main():
                    "baseline_config": args.config or None,
                    "batch_per_gpu": B, "global_batch": B * world, "env": args.env,
                    "solver": args.solver, "parallelism": f"env-shard x{world} (no collective)",
-                   "collectives": (f"RCCL process group, world {world}: barrier around the timed region, "
+                   "collectives": (f"{'gloo' if args.cpu_dry_run else 'RCCL'} process group, world {world}: "
+                                   "barrier around the timed region, "
                                    "all_gather of per-rank times, MAX all_reduce of the per-launch time"
                                    if dist.is_available() and dist.is_initialized() else None),
                    "prior": args.prior, "qp_active_frac_at_start": round(active_frac, 4),

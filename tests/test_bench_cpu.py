@@ -94,3 +94,19 @@ def test_dry_run_line_carries_the_contract_fields(cfg):
     assert rec["config"]["baseline_config"] == (cfg or None)
     # configs 2 and 5 read the materialised sigma[5, 7, 9] rows (+12 B)
     assert rf["bytes_per_env_step"] == {0: 241, 2: 253, 5: 68}[cfg]
+
+
+def test_rccl_flag_brings_up_the_group_on_one_rank():
+    """bench.py --rccl on one rank runs the N > 1 path's process-group code (rendezvous on 127.0.0.1,
+    barriers around the timed region, all_gather of the per-rank times, MAX all_reduce): over gloo in
+    the CPU dry run, over RCCL on the device (profiles/r05/bench_rccl_world1_r05z.json)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-dry-run", "--rccl", "--steps", "4",
+                        "--warmup", "1", "--batch", "256"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["n_gpus"] == 1 and rec["config"]["collectives"].startswith("gloo process group, world 1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-dry-run", "--steps", "4",
+                        "--warmup", "1", "--batch", "256"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["config"]["collectives"] is None
