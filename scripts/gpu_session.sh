@@ -146,6 +146,7 @@ for step in "$@"; do
           "k_gp_gemv<10, 1>" "$OUT/pmc_traffic_gp_gemv_rank100_B1.json" workload="GP N=3000 rank 100 B=1" \
           algorithmic_read_bytes=16724480 > /dev/null
       fi ;;
+    soak)   run soak 600 python -u -m pytest tests/test_gpu_headline_parity.py -q -rf -k soak --timeout 500 --timeout-method thread ;;
     gpm)    run gpm 300 python -u -m pytest tests/test_gpu_model.py -q -rf --timeout 200 --timeout-method thread ;;
     rccl)   run rccl 300 python bench.py --rccl --steps 20 --warmup 5 --no-cpu-baseline ;;  # the N > 1 collectives on one rank
     gvstudy)  # GEMV study variants (build/variants/librcbf_gv*.so) vs the product, GP graph bench

@@ -227,6 +227,18 @@ def test_config4_cars_B262144_vs_oracle():
     assert r["resets"] > 2000
 
 
+@pytest.mark.parametrize("mode,k,steps", [("SimulatedCars", 3, 300), ("Unicycle", 5, 1000)])
+def test_full_episode_soak_vs_oracle(mode, k, steps):
+    """A whole episode length (cars 300 steps, unicycle 1000) of config 2's /
+    config 3's batch size teacher-forced against the C oracle at every step:
+    the start states' step counters are spread over the episode, so every env
+    reaches its time limit (and resets) inside the run."""
+    B = 4096
+    r = run_teacher_forced(mode, B, steps, hazards=k)
+    assert r["resets"] >= B
+    assert r["filter_active"] > 0
+
+
 @pytest.mark.parametrize("mode,k,B", [("SimulatedCars", 3, 4096), ("Unicycle", 3, 4096), ("Unicycle", 5, 4096),
                                       ("SimulatedCars", 3, 32768), ("Unicycle", 5, 32768),
                                       ("SimulatedCars", 3, 1000)])
