@@ -76,9 +76,10 @@ def parse():
                          "all_gather and MAX all_reduce then run on the device (world size 1)")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="CPU/gloo plumbing check of the launcher (no kernel, no measurement)")
-    ap.add_argument("--launch", default="graph", choices=["graph", "seq"],
+    ap.add_argument("--launch", default="graph", choices=["graph", "seq", "aql"],
                     help="graph: hipGraph replays of --graph-steps fused steps; seq: the K launches issued from "
-                         "one host call (rcbf_safe_step_seq)")
+                         "one host call (rcbf_safe_step_seq); aql: the K dispatches as pre-built AQL packets on the "
+                         "library's own HSA queue (rcbf_aql_run, csrc/rcbf_aql.hip), one doorbell per run")
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="(internal) print the CPU baselines as JSON and exit; never touches the GPU")
     ap.add_argument("--host-cores", type=int, default=4,
@@ -111,6 +112,35 @@ def parse():
     if args.workload == "sac_update" and (args.prior == "tensor" or args.launch != "graph" or args.no_graph):
         raise SystemExit("--workload sac_update reads (B, n_s) rows or the in-kernel prior, hipGraph-launched")
     return args
+
+
+AQL_MAX_STEPS = 4096  # dispatches per AQL plan (one ring's worth: csrc/rcbf_aql.hip kQueueSize)
+
+
+def aql_dispatch_times(env, layer, ctx, graph, S):
+    """Untimed, after the timed region (--launch aql): the same S steps as a
+    profiled plan (a completion signal per dispatch on the same queue), so
+    each dispatch's start / end comes from the packet processor's own
+    timestamps (hsa_amd_profiling_get_dispatch_time, the source rocprofv3's
+    kernel trace reads).  Returns the per-dispatch durations and the period."""
+    prof = graph.queue.safe_step_plan(env, ctx["pool"], layer, steps=S, mean=ctx["mean"], sigma=ctx["sigma"],
+                                      outputs=ctx["outs"], prior_layout=ctx["layout"], profile=True)
+    prof.run(sync_hip=True)
+    t0 = time.perf_counter()
+    prof.run(sync_hip=False)
+    wall = time.perf_counter() - t0
+    t = prof.times_ns().astype(np.float64)
+    prof.free()
+    dur = (t[:, 1] - t[:, 0]) / 1e3
+    env.check_failures()
+    return {"dispatch_us_mean": round(float(dur.mean()), 4), "dispatch_us_median": round(float(np.median(dur)), 4),
+            "dispatch_us_p10_p90": [round(float(np.percentile(dur, 10)), 4), round(float(np.percentile(dur, 90)), 4)],
+            "period_us": round(float((t[-1, 1] - t[0, 0]) / 1e3 / S), 4),
+            "first_start_to_last_end_us": round(float((t[-1, 1] - t[0, 0]) / 1e3), 3),
+            "profiled_run_wall_us_per_step": round(wall * 1e6 / S, 4), "dispatches": S,
+            "how": "the timed plan's S dispatches re-run with a completion signal each on the same AQL queue "
+                   "(profiling enabled); start / end = the packet processor's dispatch timestamps "
+                   "(hsa_amd_profiling_get_dispatch_time), HSA system clock"}
 
 
 def largest_divisor_le(n, cap):
@@ -602,6 +632,12 @@ def main():
     # per fused-step launch, HIP events on the launch stream (torch's current stream)
     kern_ms = ev0.elapsed_time(ev1) / args.steps if not args.cpu_dry_run else 0.0
     env.check_failures()
+    aql_times = {}
+    if args.launch == "aql" and not args.cpu_dry_run:
+        # no HIP stream carries the AQL dispatches: the per-launch duration comes from the packet processor's
+        # dispatch timestamps of the same S steps, re-run profiled right after the timed region
+        aql_times = aql_dispatch_times(env, layer, ctx, graph, S)
+        kern_ms = aql_times["dispatch_us_mean"] / 1e3
     per_rank_s = shard.gather_over_ranks(el, world, dev)
     el = max(per_rank_s)
     kern_ms = shard.max_over_ranks(kern_ms, world, dev)
@@ -621,7 +657,9 @@ def main():
         extra = extra_measurements(env, layer, dev, args)
     hz = f"{args.hazards}-hazard " if args.env == "Unicycle" else ""
     launch = ("no kernel (CPU dry run)" if args.cpu_dry_run else "eager launches" if args.no_graph
-              else f"{S} launches from one host call" if args.launch == "seq" else f"hipGraph of {S} steps")
+              else f"{S} launches from one host call" if args.launch == "seq"
+              else f"{S} AQL dispatches per run on the library's HSA queue" if args.launch == "aql"
+              else f"hipGraph of {S} steps")
     sac = args.workload == "sac_update"
     prior_text = {"prior": "prior mean/sigma in-kernel",
                   "tensor": "per-env mean/sigma, column layout of rcbf_gp_predict_cols",
@@ -691,6 +729,12 @@ def main():
                                            "per dispatch); frac_rocprof is a traced figure, frac the untraced one")
     if span:
         rec["roofline"]["span"] = span
+    if aql_times:
+        rec["roofline"]["aql_dispatch_times"] = aql_times
+        rec["roofline"]["timing"] = ("achieved = bytes_per_launch / kernel_ms; kernel_ms = the mean dispatch duration "
+                                     "(packet processor timestamps) of the timed plan's steps re-run profiled on the "
+                                     "same queue (aql_dispatch_times); host_submit_ms = host time of the timed run "
+                                     "call (submission AND the wait for completion)")
     if world > 1:  # the spread of the timed region over ranks (value is set by the slowest)
         ms = sorted(v / args.steps * 1e3 for v in per_rank_s)
         rec["per_rank_ms"] = {"min": round(ms[0], 5), "median": round(float(np.median(ms)), 5),
@@ -744,7 +788,8 @@ def setup_gpu(args, dev, rank, B):
         env = BatchedUnicycleEnv(B, device=dev, seed=1234, env_offset=shard.env_offset(rank, B),
                                  hazards_locations=unicycle_hazards(args.hazards))
     layer = CBFQPLayer(env, LArgs(), gamma_b=20.0, solver=solver)
-    S = args.steps if args.launch == "seq" else largest_divisor_le(args.steps, args.graph_steps)
+    S = (args.steps if args.launch == "seq" or (args.launch == "aql" and args.steps <= AQL_MAX_STEPS)
+         else largest_divisor_le(args.steps, AQL_MAX_STEPS if args.launch == "aql" else args.graph_steps))
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
     init_states(env, gen, args.env)
@@ -785,6 +830,20 @@ def setup_gpu(args, dev, rank, B):
             def replay(self):
                 steps(S)
         graph = _Eager()
+    elif args.launch == "aql":
+        from rcbf_amd.aql import AqlQueue
+        queue = AqlQueue(dev, profile=True)
+        plan = queue.safe_step_plan(env, pool, layer, steps=S, mean=mean, sigma=sigma, outputs=outs,
+                                    prior_layout=layout)
+
+        class _Aql:
+            def replay(self):
+                plan.run(sync_hip=False)  # the timed region synchronises the device before it starts
+        graph = _Aql()
+        graph.queue, graph.plan = queue, plan
+        for _ in range(2):
+            graph.replay()
+        untimed += 2 * S
     else:
         graph = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=dev)
@@ -1174,7 +1233,7 @@ def cascade_rows(dev):
 
         def launch():
             lib.rcbf_cascade_u_safe(ctypes.byref(layer._prm), B, _lib.ptr(U), _lib.ptr(X), _lib.ptr(M), _lib.ptr(S),
-                                    _lib.ptr(o), None, _lib.ptr(flag), _lib.stream_of(dev))
+                                    _lib.ptr(o), None, _lib.ptr(flag), None, _lib.stream_of(dev))
         ms = _time_graph(launch, 50, dev)
         nbytes = B * 8 * (n_u + 3 * n_s + n_u)
         out[f"cascade_u_safe_{name}_B{B}"] = {"us": round(ms * 1e3, 2), "qps_per_s": round(B / ms * 1e3, 1),

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RCBF_ABI_VERSION 11
+#define RCBF_ABI_VERSION 12
 
 /* dynamics modes: rcbf_sac/dynamics.py:22-23 DYNAMICS_MODE */
 #define RCBF_MODE_SIMULATED_CARS 0
@@ -57,6 +57,9 @@ extern "C" {
 #define RCBF_E_BAD_MODE 1001
 #define RCBF_E_BAD_SHAPE 1002
 #define RCBF_E_NULL 1003
+#define RCBF_E_HSA 1004     /* an HSA runtime call failed, or the AQL queue reported an error */
+#define RCBF_E_TIMEOUT 1005 /* rcbf_aql_run: the dispatches did not complete in time */
+#define RCBF_E_GP_HANDOFF 1006 /* rcbf_gp_workspace_check: a GEMV call found a non-zero arrival counter */
 
 #define RCBF_MAX_HAZARDS 8
 
@@ -203,11 +206,14 @@ int rcbf_safe_action_apply_jac(int64_t B, int32_t n_u, const double* jac, const 
                                float* grad_u_rl, hipStream_t stream);
 
 /* CascadeCBFLayer.get_u_safe (cbf_qp.py:29-53), fp64 batched: build ->
- * normalise -> exact QP.  Returns u_qp only (caller adds u_nom, no clamp). */
+ * normalise -> exact QP.  Returns u_qp only (caller adds u_nom, no clamp);
+ * eps_out [nullable] (B,) f64 receives the slack epsilon, the QP solution's
+ * last component (sol[0][-1], which the reference checks against 0.1 at
+ * cbf_qp.py:283-284). */
 int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom,
                         const double* x, const double* mu, const double* sigma,
                         double* u_safe_out, int32_t* status_out, int32_t* fail_flag,
-                        hipStream_t stream);
+                        double* eps_out, hipStream_t stream);
 
 /* ---------------------------------------------------------------------- */
 /* GP disturbance posterior                              */
@@ -243,8 +249,23 @@ typedef struct rcbf_gp_model {
 /* Floats of workspace rcbf_gp_predict needs for B queries.  Its first words
  * are the arrival counters of the one-launch GEMV path (B <= 8): a workspace
  * must be ZERO-FILLED before its first use (e.g. torch.zeros); every call
- * leaves those words zero again.  One workspace per concurrent call. */
+ * leaves those words zero again.  One workspace per concurrent call (per
+ * stream); rcbf_gp_workspace_check detects a violation after the fact. */
 int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B);
+
+/* Zero the workspace's counter words (hipMemsetAsync on `stream`): the
+ * initialisation a new workspace needs before its first rcbf_gp_predict. */
+int rcbf_gp_workspace_init(const rcbf_gp_model* m, float* workspace, hipStream_t stream);
+
+/* SYNCHRONOUS check of the one-launch GEMV hand-off (waits for `stream`): a
+ * GEMV workgroup that draws an arrival ticket past its block's (or GP's)
+ * arrival count proves the counter was not zero when its call started -- the
+ * workspace was not zero-filled, a call was aborted part-way, or two calls
+ * shared the workspace at once -- and sets the workspace's fail word; the
+ * outputs of such a call are not valid.  Returns RCBF_E_GP_HANDOFF if the word
+ * is set, after zeroing every counter and the word (the next call is clean);
+ * 0 otherwise. */
+int rcbf_gp_workspace_check(const rcbf_gp_model* m, float* workspace, hipStream_t stream);
 
 /* DynamicsModel.predict_disturbance(test_x) with fitted GPs (dynamics.py:
  * 342-390, gp_model.py:86-114): x (B, n_s) f32 states -> mean (B, n_s) and
@@ -446,6 +467,59 @@ int rcbf_safe_rollout(const rcbf_params* prm, int64_t B, int32_t K, double* x, d
                       int32_t* step, uint32_t* episode, const float* u_rl, float* obs_out,
                       float* reward_sum, float* cost_sum, int32_t* n_done, int32_t* fail_flag,
                       uint64_t seed, int64_t env_offset, hipStream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* The fused safe step on a user-mode AQL queue of the library's own
+ * (csrc/rcbf_aql.hip).  Same kernels, same machine code as rcbf_safe_step --
+ * the gfx950 code object of rcbf_env.o, unbundled at build time into
+ * librcbf_steps.co -- dispatched as pre-built AQL packets instead of through
+ * the HIP launch path, so K steps cost ~1 us of host time instead of a
+ * hipGraph launch (~16-25 us host, ~17 us before the first kernel starts) or
+ * K hipLaunchKernel calls (~5 us each).
+ *
+ * Replaces: env.step() of the batched env in the SAC loop (main.py:93-95 with
+ * sac_cbf.py:218-238), K steps per call; like a gym step the call is
+ * SYNCHRONOUS: rcbf_aql_run returns after the K steps have completed.  The
+ * queue is not a HIP stream: the caller orders it against HIP work by
+ * synchronising before the run (inputs written by HIP kernels must be
+ * complete); HIP work issued after the run sees its results.
+ *
+ * rcbf_aql_open: device = HIP device ordinal; code_object [nullable] = path
+ * of librcbf_steps.co (NULL: next to librcbf_hip.so); flags RCBF_AQL_PROFILE
+ * enables per-dispatch timestamps (hsa_amd_profiling) on the queue.  One
+ * producer thread per queue.
+ * rcbf_aql_safe_step_plan: the arguments of rcbf_safe_step_seq (prior_cols =
+ * 1: the column layout of rcbf_safe_step_cols) plus span_out [nullable] (the
+ * measurement instantiation of rcbf_safe_step_span; step j writes its stamps
+ * to span_out[2 ceil(B/64) j ...], K blocks of rcbf_safe_step_span's layout); the K
+ * kernel-argument blocks are copied to device memory here (synchronous), so
+ * the buffers must stay allocated while the plan exists.  flags
+ * RCBF_AQL_PROFILE: a completion signal per dispatch, read back with
+ * rcbf_aql_plan_times (start, end in ns of the HSA system clock per step).
+ * rcbf_aql_run: submit the K dispatches (barrier bit on each), ring the
+ * doorbell once, busy-wait for completion; timeout_us 0 -> 10 s.
+ * Returns RCBF_E_HSA / RCBF_E_TIMEOUT on a queue error or a timeout. */
+#define RCBF_AQL_PROFILE 1
+/* plan flags: memory-fence scopes of the first / last packet (default: system
+ * scope at both ends, agent scope between steps) */
+#define RCBF_AQL_FIRST_ACQUIRE_AGENT 2 /* the first step acquires at agent scope */
+#define RCBF_AQL_LAST_RELEASE_AGENT 4  /* the last step releases at agent scope */
+#define RCBF_AQL_STUDY_MID_NOFENCE 8   /* STUDY ONLY: no fences between steps (not coherent across XCDs) */
+#define RCBF_AQL_SAFE_STEP_KERNARG_BYTES 408 /* sizeof the k_safe_step argument block */
+typedef struct rcbf_aql rcbf_aql;
+typedef struct rcbf_aql_plan rcbf_aql_plan;
+int rcbf_aql_open(int32_t device, const char* code_object, int32_t flags, rcbf_aql** out);
+int rcbf_aql_close(rcbf_aql* q);
+int rcbf_aql_kernel_count(const rcbf_aql* q);
+int rcbf_aql_safe_step_plan(rcbf_aql* q, const rcbf_params* prm, int64_t B, int32_t K, double* x, double* aux,
+                            int32_t* step, uint32_t* episode, const float* const* u_rl_seq, int32_t n_u_rl,
+                            const float* mu, const float* sigma, int32_t prior_cols, float* obs_out, float* u_out,
+                            float* reward, float* cost, uint8_t* done, uint8_t* goal_met, int32_t* status_out,
+                            int32_t* fail_flag, int32_t auto_reset, uint64_t seed, int64_t env_offset,
+                            uint64_t* span_out, int32_t flags, rcbf_aql_plan** out);
+int rcbf_aql_run(rcbf_aql_plan* plan, uint64_t timeout_us);
+int rcbf_aql_plan_times(const rcbf_aql_plan* plan, uint64_t* start_end_ns);
+int rcbf_aql_plan_free(rcbf_aql_plan* plan);
 
 /* ---------------------------------------------------------------------- */
 const char* rcbf_version(void);

@@ -10,7 +10,8 @@ template <int SOLVER, int MODE, int K>
 __global__ void __launch_bounds__(kBlock) k_cascade(rcbf_params prm, int64_t B, const double* __restrict__ un,
                                                     const double* __restrict__ x, const double* __restrict__ mu,
                                                     const double* __restrict__ sigma, double* __restrict__ u_out,
-                                                    int32_t* __restrict__ status_out, int32_t* fail_flag) {
+                                                    int32_t* __restrict__ status_out, int32_t* fail_flag,
+                                                    double* __restrict__ eps_out) {
     using D = Dims<MODE, K>;
     int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= B) return;
@@ -44,6 +45,7 @@ __global__ void __launch_bounds__(kBlock) k_cascade(rcbf_params prm, int64_t B, 
         qp_solve<SOLVER, D::N, D::M, true, double>(pm, q, G, h, prm.max_iter, prm.eps, res);
 #pragma unroll
     for (int c = 0; c < D::NU; ++c) u_out[i * D::NU + c] = res.z[c];
+    if (eps_out) eps_out[i] = res.z[D::NU];  // the slack, sol[0][-1] (cbf_qp.py:278, 283-284)
     report(res.status, status_out, i, fail_flag);
 }
 
@@ -53,13 +55,13 @@ extern "C" {
 
 int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom, const double* x, const double* mu,
                         const double* sigma, double* u_safe_out, int32_t* status_out, int32_t* fail_flag,
-                        hipStream_t stream) {
+                        double* eps_out, hipStream_t stream) {
     if (int e = check_prm(prm)) return e;
     if (B < 0) return RCBF_E_BAD_SHAPE;
     if (B == 0) return 0;
     if (!x || !u_nom || !u_safe_out) return RCBF_E_NULL;
     RCBF_DISPATCH(prm, hipLaunchKernelGGL((k_cascade<SOLVER_, MODE_, K_>), dim3(grid_for(B)), dim3(kBlock), 0, stream,
-                                          *prm, B, u_nom, x, mu, sigma, u_safe_out, status_out, fail_flag));
+                                          *prm, B, u_nom, x, mu, sigma, u_safe_out, status_out, fail_flag, eps_out));
     return launch_status();
 }
 

@@ -432,10 +432,15 @@ inline int gp_gv_tiles(const rcbf_gp_model& m) {
 // counter words at the start of the workspace: n_s * n_cb block counters, then n_s GP counters, each
 // on a 128-B line of its own -- arrivals on one line serialise at the memory-side atomic unit (~13 ns
 // each): with the 10 GPs' counters in one line, rank 100 at B = 1 spent ~13 us of its 18 there (r05e)
+// The line after them holds the hand-off's fail word: a workgroup whose ticket is past its block's (or
+// GP's) arrival count proves the counter was not zero when the call started (a workspace that was not
+// zero-filled, a call aborted part-way, or two calls sharing one workspace at once) and sets bit 0;
+// rcbf_gp_workspace_check reports it and zeroes the counters.
 constexpr int kGvCtrStride = 32;  // words
-inline int64_t gp_counter_words(const rcbf_gp_model& m) {
+__host__ __device__ inline int64_t gp_fail_word(const rcbf_gp_model& m) {
     return (int64_t)m.n_s * (m.C_pad / kGpCols + 1) * kGvCtrStride;
 }
+inline int64_t gp_counter_words(const rcbf_gp_model& m) { return gp_fail_word(m) + kGvCtrStride; }
 
 struct GpCols {
     int32_t n;
@@ -629,7 +634,11 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
     // 6. arrival at block (i, cb): the last of its tiles reduces the block
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t == 0) s_last = ticket(&counters[(i * n_cb + cb) * kGvCtrStride]) == (unsigned)(nrc - 1);
+    if (t == 0) {
+        const unsigned tk = ticket(&counters[(i * n_cb + cb) * kGvCtrStride]);
+        if (tk >= (unsigned)nrc) atomicOr(&counters[gp_fail_word(m)], 1u);  // the counter was not zero at entry
+        s_last = tk == (unsigned)(nrc - 1);
+    }
     __syncthreads();
     if (!s_last) return;
     const int r_rank = m.r;
@@ -691,7 +700,9 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
     __syncthreads();
     if (t == 0) {
         atomicExch(&counters[(i * n_cb + cb) * kGvCtrStride], 0u);  // consumed: zero for the next call
-        s_last = ticket(&counters[(m.n_s * n_cb + i) * kGvCtrStride]) == (unsigned)(n_cb - 1);
+        const unsigned tk = ticket(&counters[(m.n_s * n_cb + i) * kGvCtrStride]);
+        if (tk >= (unsigned)n_cb) atomicOr(&counters[gp_fail_word(m)], 1u);
+        s_last = tk == (unsigned)(n_cb - 1);
     }
     __syncthreads();
     if (!s_last) return;
@@ -845,6 +856,27 @@ int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B) {
     return cw + (int64_t)m->n_s * (2 * n_cb + 1) * B + (sk > 1 ? (int64_t)sk * m->n_s * B * m->C_pad : 0);
 }
 
+int rcbf_gp_workspace_init(const rcbf_gp_model* m, float* workspace, hipStream_t stream) {
+    if (!m || !workspace) return RCBF_E_NULL;
+    if (m->C_pad < kGpCols || m->n_s < 1) return RCBF_E_BAD_SHAPE;
+    return (int)hipMemsetAsync(workspace, 0, (size_t)gp_counter_words(*m) * 4, stream);
+}
+
+int rcbf_gp_workspace_check(const rcbf_gp_model* m, float* workspace, hipStream_t stream) {
+    if (!m || !workspace) return RCBF_E_NULL;
+    if (m->C_pad < kGpCols || m->n_s < 1) return RCBF_E_BAD_SHAPE;
+    unsigned fail = 0;
+    int rc = (int)hipMemcpyAsync(&fail, reinterpret_cast<unsigned*>(workspace) + gp_fail_word(*m), 4,
+                                 hipMemcpyDeviceToHost, stream);
+    if (!rc) rc = (int)hipStreamSynchronize(stream);
+    if (rc) return rc;
+    if (!fail) return 0;
+    // the hand-off saw a non-zero counter: zero every counter and the fail word, so the next call is clean
+    rc = rcbf_gp_workspace_init(m, workspace, stream);
+    if (!rc) rc = (int)hipStreamSynchronize(stream);
+    return rc ? rc : RCBF_E_GP_HANDOFF;
+}
+
 int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out, float* std_out,
                     float* workspace, hipStream_t stream) {
     if (!mean_out || !std_out) return RCBF_E_NULL;
@@ -871,7 +903,9 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
         !m->outscale || !m->noise || !m->y_scale)
         return RCBF_E_NULL;
     const int n_cb = m->C_pad / kGpCols;
-    // the arrival counters of the GEMV path sit first (zero-filled by the caller once, left zero by every call)
+    // the arrival counters of the GEMV path sit first (zero-filled by the caller once -- torch.zeros or
+    // rcbf_gp_workspace_init -- and left zero by every call; a call that finds one non-zero sets the fail
+    // word rcbf_gp_workspace_check reads)
     unsigned* counters = reinterpret_cast<unsigned*>(workspace);
     float* ws = workspace + gp_counter_words(*m);
     if (B <= kGvMaxB) {

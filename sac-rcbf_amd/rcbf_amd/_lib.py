@@ -23,9 +23,10 @@ SOLVER_PDIPM = 1
 SOLVER_GI = 2
 QP_OK, QP_MAX_ITER, QP_INFEASIBLE, QP_NONFINITE = 0, 1, 2, 3
 MAX_HAZARDS = 8
-ABI_VERSION = 11
+ABI_VERSION = 12
 
-_ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL"}
+_ERRORS = {1001: "RCBF_E_BAD_MODE", 1002: "RCBF_E_BAD_SHAPE", 1003: "RCBF_E_NULL", 1004: "RCBF_E_HSA",
+           1005: "RCBF_E_TIMEOUT", 1006: "RCBF_E_GP_HANDOFF"}
 
 
 class RcbfParams(ctypes.Structure):
@@ -85,6 +86,8 @@ SIGNATURES = {
     "rcbf_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_obs_safe_action": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_gp_workspace_floats": [_GPM, _I64],
+    "rcbf_gp_workspace_init": [_GPM, _P, _P],
+    "rcbf_gp_workspace_check": [_GPM, _P, _P],
     "rcbf_predict_next_state": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P],
     "rcbf_model_step": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _U64, _U64, _P, _P, _P, _P, _P],
     "rcbf_state_from_obs": [_PRM, _I64, _P, _P, _P],
@@ -96,7 +99,7 @@ SIGNATURES = {
     "rcbf_safe_action_jac": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_obs_safe_action_jac": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_safe_action_apply_jac": [_I64, _I32, _P, _P, _P, _P],
-    "rcbf_cascade_u_safe": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_cascade_u_safe": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_env_reset": [_PRM, _I64, _P, _P, _U64, _I64, _P, _P, _P, _P, _P, _P],
     "rcbf_env_step": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
     "rcbf_safe_step": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
@@ -111,6 +114,15 @@ SIGNATURES = {
                             _I64, _P, _P],
     "rcbf_env_step_sync": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _I32, _U64, _I64, _P],
     "rcbf_host_alloc": [_I64, ctypes.POINTER(ctypes.c_void_p)],
+    # the AQL dispatch path (csrc/rcbf_aql.hip; rcbf_amd.aql)
+    "rcbf_aql_open": [_I32, ctypes.c_char_p, _I32, ctypes.POINTER(ctypes.c_void_p)],
+    "rcbf_aql_close": [_P],
+    "rcbf_aql_kernel_count": [_P],
+    "rcbf_aql_safe_step_plan": [_P, _PRM, _I64, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _P,
+                                _P, _P, _I32, _U64, _I64, _P, _I32, ctypes.POINTER(ctypes.c_void_p)],
+    "rcbf_aql_run": [_P, _U64],
+    "rcbf_aql_plan_times": [_P, _P],
+    "rcbf_aql_plan_free": [_P],
     "rcbf_host_free": [_P],
     "rcbf_version": [],
     "rcbf_abi_version": [],

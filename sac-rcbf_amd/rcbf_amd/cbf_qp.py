@@ -3,7 +3,9 @@
 get_u_safe builds the fp64 rows, normalises them and solves the QP exactly
 (Goldfarb-Idnani, the algorithm of the quadprog call at cbf_qp.py:276) in one
 launch of rcbf_cascade_u_safe.  It also accepts a batch (leading axis).
-The reference's per-call print of the quadprog result (:278) is not kept.
+The reference's per-call print of the quadprog result (:278) is not kept;
+its slack-violation warning (:283-284) is: any row whose slack |epsilon|
+exceeds 0.1 prints the reference's message (get_u_safe and solve_qp).
 """
 import ctypes
 
@@ -13,6 +15,14 @@ import torch
 from . import _lib
 from .dynamics import DYNAMICS_MODE
 from .params import make_params
+
+
+def _warn_slack(eps):
+    """cbf_qp.py:283-284: the reference's warning when the QP needed a slack
+    |epsilon| > 0.1 (one line per such row)."""
+    for e in np.asarray(eps, np.float64).reshape(-1):
+        if np.abs(e) > 1e-1:
+            print('CBF indicates constraint violation might occur. epsilon = {}'.format(e))
 
 
 class CascadeCBFLayer:
@@ -42,13 +52,17 @@ class CascadeCBFLayer:
         U, X, M, S = d(un), d(s), d(mean_pred), d(sigma)
         B = X.shape[0]
         out = torch.empty(B, U.shape[1], dtype=torch.float64, device=dev)
+        eps = torch.empty(B, dtype=torch.float64, device=dev)
         flag = torch.zeros(1, dtype=torch.int32, device=dev)
         rc = _lib.load().rcbf_cascade_u_safe(ctypes.byref(self._prm), B, _lib.ptr(U), _lib.ptr(X), _lib.ptr(M),
-                                             _lib.ptr(S), _lib.ptr(out), None, _lib.ptr(flag), _lib.stream_of(dev))
+                                             _lib.ptr(S), _lib.ptr(out), None, _lib.ptr(flag), _lib.ptr(eps),
+                                             _lib.stream_of(dev))
         _lib.check(rc, "rcbf_cascade_u_safe")
         if int(flag.item()):
             raise ValueError("constraints are inconsistent, no solution")  # quadprog's ValueError (:279-281)
         res = out.cpu().numpy()
+        self.last_eps = eps.cpu().numpy()
+        _warn_slack(self.last_eps)
         return res[0] if single else res
 
     def get_cbf_qp_constraints(self, u_nom, state, mean_pred, sigma_pred):
@@ -103,7 +117,9 @@ class CascadeCBFLayer:
         _lib.check(rc, "rcbf_qp_solve_f64")
         if int(flag.item()):
             raise ValueError("constraints are inconsistent, no solution")
-        return z[0, :-1].cpu().numpy()
+        zh = z[0].cpu().numpy()
+        _warn_slack(zh[-1:])
+        return zh[:-1]
 
     def get_cbfs(self, hazards_locations, hazards_radius):
         """cbf_qp.py:288-323: (get_h, get_dhdx) of the hazard CBFs

@@ -20,6 +20,45 @@ DYNAMICS_MODE = {"Unicycle": {"n_s": 3, "n_u": 2},
 MAX_STD = {"Unicycle": [2e-1, 2e-1, 2e-1], "SimulatedCars": [0, 0.2, 0, 0.2, 0, 0.2, 0, 0.2, 0, 0.2]}
 
 
+# gpytorch state_dict keys of the reference's GP (gp_model.py:12-27: ScaleKernel(RBFKernel), GaussianLikelihood)
+_REF_NOISE = "likelihood.noise_covar.raw_noise"
+_REF_OS = "covar_module.raw_outputscale"
+_REF_LS = "covar_module.base_kernel.raw_lengthscale"
+
+
+def _load_weights_only(path):
+    """torch.load with the restricted (weights-only) unpickler; numpy arrays
+    (the reference torch.saves its training data as ndarrays) are allowed
+    through numpy's own array reconstruction, nothing else."""
+    try:
+        return torch.load(path, weights_only=True, map_location="cpu")
+    except Exception:
+        try:
+            from numpy._core.multiarray import _reconstruct
+        except ImportError:  # numpy 1.x
+            from numpy.core.multiarray import _reconstruct
+        allowed = [_reconstruct, np.ndarray, np.dtype] + [type(np.dtype(t)) for t in (np.float64, np.float32,
+                                                                                      np.int64, np.int32)]
+        with torch.serialization.safe_globals(allowed):
+            return torch.load(path, weights_only=True, map_location="cpu")
+
+
+def _as_numpy(v):
+    return v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)
+
+
+def _gpytorch_hyper(sd):
+    """(lengthscale, outputscale, noise) of one reference GP state_dict:
+    gpytorch's constraint transforms, softplus(raw) + lower bound (the noise's
+    GreaterThan(1e-4) bound when the state_dict does not carry it)."""
+    def val(key, default_lb):
+        raw = float(torch.as_tensor(sd[key], dtype=torch.float64).reshape(-1)[0])
+        lb_key = key + "_constraint.lower_bound"
+        lb = float(torch.as_tensor(sd[lb_key], dtype=torch.float64).reshape(-1)[0]) if lb_key in sd else default_lb
+        return float(torch.nn.functional.softplus(torch.tensor(raw, dtype=torch.float64))) + lb
+    return val(_REF_LS, 0.0), val(_REF_OS, 0.0), val(_REF_NOISE, 1e-4)
+
+
 class DynamicsModel:
     """DynamicsModel with the reference's constructor and methods; the GP
     disturbance estimators are one rcbf_amd.gp.GPDisturbanceModel on the device."""
@@ -44,6 +83,14 @@ class DynamicsModel:
         if self.gp_variance not in ("love", "exact"):
             raise ValueError(f"gp_variance must be 'love' or 'exact', got {self.gp_variance!r}")
         self.gp_rank = getattr(args, "gp_rank", None)
+        # the mean's solve: "cg" (default) is gpytorch's eval-mode solve the reference predicts with
+        # (preconditioned CG at tolerance 0.01 above 800 points, gp.cg_mean_solve); "exact" the Cholesky solve
+        self.gp_mean = getattr(args, "gp_mean", "cg")
+        if self.gp_mean not in ("cg", "exact"):
+            raise ValueError(f"gp_mean must be 'cg' or 'exact', got {self.gp_mean!r}")
+        # LOVE's Lanczos start vectors come from this generator (seeded by seed()), not torch's global stream
+        self._love_gen = torch.Generator()
+        self._love_gen.manual_seed(torch.initial_seed() & 0xFFFFFFFFFFFF)
         if hasattr(args, "l_p"):
             self.l_p = args.l_p
         self.device = torch.device("cuda" if getattr(args, "cuda", False) else "cpu")
@@ -87,7 +134,8 @@ class DynamicsModel:
             train_x = self.disturbance_history["state"]
             train_y = self.disturbance_history["disturbance"]
         self.disturb_estimators = gp.fit(train_x, train_y, MAX_STD[self.env.dynamics_mode], training_iter,
-                                         rank=self._gp_factor_rank(len(train_x)))
+                                         rank=self._gp_factor_rank(len(train_x)), mean_solve=self.gp_mean,
+                                         love_generator=self._love_gen)
         self.train_x = np.array(train_x, copy=True)
         self.train_y = np.array(train_y, copy=True)
 
@@ -108,9 +156,11 @@ class DynamicsModel:
         values, not as a gpytorch state_dict (gpytorch is not used here)."""
         if not self.disturb_estimators or self.train_x is None or self.train_y is None:
             return
+        raw = bool(getattr(self.disturb_estimators, "raw_train", False))
         weights = [{"lengthscale": torch.tensor(h[0], dtype=torch.float64),
                     "outputscale": torch.tensor(h[1], dtype=torch.float64),
-                    "noise": torch.tensor(h[2], dtype=torch.float64)} for h in self.disturb_estimators.hyper]
+                    "noise": torch.tensor(h[2], dtype=torch.float64),
+                    "raw_train": torch.tensor(raw)} for h in self.disturb_estimators.hyper]
         torch.save(weights, f"{output}/gp_models.pkl")
         torch.save(torch.as_tensor(self.train_x), f"{output}/gp_models_train_x.pkl")
         torch.save(torch.as_tensor(self.train_y), f"{output}/gp_models_train_y.pkl")
@@ -118,25 +168,48 @@ class DynamicsModel:
             torch.save(self.disturb_estimators.love_init, f"{output}/gp_models_love_init.pkl")
 
     def load_disturbance_models(self, output):
-        """Restores what save_disturbance_models wrote (None -> no-op); any
+        """Restores what save_disturbance_models wrote, or what the REFERENCE's
+        save_disturbance_models wrote (dynamics.py:392-419: per GP a gpytorch
+        state_dict, the training data as numpy arrays); None -> no-op; any
         failure raises Exception('Could not load GP models from ...') like the
-        reference."""
+        reference.  Every file goes through torch.load(weights_only=True) (the
+        restricted unpickler; numpy's array reconstruction is the one global
+        it is allowed beyond tensors, for the reference's training data).
+
+        A reference checkpoint's hyperparameters are its raw parameters through
+        gpytorch's constraints: noise = softplus(raw_noise) + its lower bound
+        (GreaterThan(1e-4)), lengthscale / outputscale = softplus(raw) (+ their
+        bounds, 0 by default).  The reference rebuilds the loaded GPs on the
+        RAW saved training data (GPyDisturbanceEstimator(self.train_x,
+        self.train_y[:, i]), :401-403) while it fits them on normalised data
+        and still normalises the queries (:371-380); the loaded model keeps
+        that behaviour.  Parity unpinned (gpytorch is not installed; the test
+        builds such a checkpoint from synthetic raw parameters)."""
         if output is None:
             return
         from . import gp
         self.disturb_estimators = None
         try:
-            weights = torch.load(f"{output}/gp_models.pkl", weights_only=True)
-            tx = torch.load(f"{output}/gp_models_train_x.pkl", weights_only=True).cpu().numpy()
-            ty = torch.load(f"{output}/gp_models_train_y.pkl", weights_only=True).cpu().numpy()
-            hyper = [(float(w["lengthscale"]), float(w["outputscale"]), float(w["noise"])) for w in weights]
+            weights = _load_weights_only(f"{output}/gp_models.pkl")
+            tx = np.asarray(_as_numpy(_load_weights_only(f"{output}/gp_models_train_x.pkl")), np.float64)
+            ty = np.asarray(_as_numpy(_load_weights_only(f"{output}/gp_models_train_y.pkl")), np.float64)
+            reference_format = all(_REF_LS in w for w in weights)
+            if reference_format:
+                hyper = [_gpytorch_hyper(w) for w in weights]
+                raw_train = True
+            else:
+                hyper = [(float(w["lengthscale"]), float(w["outputscale"]), float(w["noise"])) for w in weights]
+                raw_train = bool(weights[0].get("raw_train", False))
             if len(hyper) != self.n_s:
                 raise ValueError("state dimension mismatch")
             import os
             init_path = f"{output}/gp_models_love_init.pkl"
-            init = torch.load(init_path, weights_only=True) if os.path.exists(init_path) else None
-            self.disturb_estimators = gp.GPDisturbanceModel(tx, ty, hyper, rank=self._gp_factor_rank(len(tx)),
-                                                            love_init=init)
+            init = _load_weights_only(init_path) if os.path.exists(init_path) else None
+            dev = self.device if self.device.type == "cpu" else None
+            self.disturb_estimators = gp.GPDisturbanceModel(tx, ty, hyper, device=dev,
+                                                            rank=self._gp_factor_rank(len(tx)), love_init=init,
+                                                            mean_solve=self.gp_mean, love_generator=self._love_gen,
+                                                            raw_train=raw_train)
             self.train_x, self.train_y = tx, ty
         except Exception:
             raise Exception("Could not load GP models from {}".format(output))
@@ -145,6 +218,7 @@ class DynamicsModel:
         torch.manual_seed(s)
         if torch.cuda.is_available():
             torch.cuda.manual_seed(s)
+        self._love_gen.manual_seed(s)
 
     # -- obs <-> state (dynamics.py:190-261) -------------------------------
     def _state_from_obs_device(self, obs):
@@ -161,17 +235,23 @@ class DynamicsModel:
             prm.num_hazards = 1 if prm.mode == _lib.MODE_UNICYCLE else 0
         o = obs.contiguous()
         out = torch.empty(o.shape[0], self.n_s, dtype=torch.float32, device=o.device)
-        rc = _lib.load().rcbf_state_from_obs(ctypes.byref(prm), o.shape[0], _lib.ptr(o), _lib.ptr(out),
-                                             _lib.stream_of(o.device))
+        with torch.cuda.device(o.device):
+            rc = _lib.load().rcbf_state_from_obs(ctypes.byref(prm), o.shape[0], _lib.ptr(o), _lib.ptr(out),
+                                                 _lib.stream_of(o.device))
         _lib.check(rc, "rcbf_state_from_obs")
         return out
+
+    _N_OBS = {"SimulatedCars": 10, "Unicycle": 7}
 
     def get_state(self, obs):
         expand = len(obs.shape) == 1
         if torch.is_tensor(obs) and obs.is_cuda and obs.dtype == torch.float32:
             o = obs.unsqueeze(0) if expand else obs
-            s = self._state_from_obs_device(o)
-            return s.squeeze(0) if expand else s
+            # the kernel reads whole (B, n_o) rows at the env's observation width: anything else (e.g. a
+            # (B, 4) unicycle row or a state tensor) takes the torch path below, as the reference accepts it
+            if o.dim() == 2 and o.shape[1] == self._N_OBS[self.env.dynamics_mode]:
+                s = self._state_from_obs_device(o)
+                return s.squeeze(0) if expand else s
         if torch.is_tensor(obs):
             o = obs.unsqueeze(0) if expand else obs
             # the reference rescales in fp64 numpy then casts back to obs.dtype

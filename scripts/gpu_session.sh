@@ -64,6 +64,14 @@ for step in "$@"; do
     bench)  run bench 600 python bench.py ;;
     driver) run driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
     benchx) run benchx 600 python bench.py --extra --no-cpu-baseline ;;
+    aqltest) run aqltest 300 python -u -m pytest tests/test_gpu_aql.py -q -rf --timeout 200 --timeout-method thread ;;
+    aqltl) run aqltl 300 python -u scripts/exp_aql_timeline.py ;;
+    drvaql) run drvaql 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --launch aql ;;
+    benchaql) run benchaql 300 python bench.py --no-cpu-baseline --launch aql ;;
+    profdrvaql)  # the driver's command with the AQL launch, traced (rocprofv3 intercepts the library's HSA queue too)
+      run profdrvaql 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profdrvaql" -o run -- \
+        python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --launch aql
+      [ -f "$OUT/profdrvaql/run_kernel_stats.csv" ] && cp "$OUT/profdrvaql/run_kernel_stats.csv" "$OUT/kernel_stats_driver_form_aql_cars_B65536_$TAG.csv" ;;
     sweep)  # waves per SIMD: B = 32768 (half the SIMDs), 65536 (one wave each), 98304, 131072 (two)
       for w in cars uni3 uni5; do for b in 32768 65536 98304 131072; do
         run "sweep_${w}_$b" 300 python bench.py --no-cpu-baseline --batch "$b" $(wl_args "$w")

@@ -234,3 +234,49 @@ def test_header_constants_match_the_python_mirror():
     import struct
     v = struct.unpack("<d", struct.pack("<Q", _lib.JAC_NO_GRAD))[0]
     assert v != v and _lib.JAC_NO_GRAD != 0x7FF8000000000000  # a NaN, not the canonical one
+
+
+def _steps_code_object_kernels():
+    """AMDGPU metadata of librcbf_steps.co (the code object the AQL path
+    loads; built by __graft_entry__.build from rcbf_env.o)."""
+    import subprocess
+
+    import yaml
+    co = os.path.join(ROOT, "sac-rcbf_amd", "rcbf_amd", "librcbf_steps.co")
+    if not os.path.exists(co):
+        pytest.skip("librcbf_steps.co not built")
+    txt = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                         text=True).stdout
+    m = re.search(r"^\s*---\n(.*?)^\.\.\.", txt, re.S | re.M)
+    assert m, "no AMDGPU metadata in librcbf_steps.co"
+    return yaml.safe_load(m.group(1))["amdhsa.kernels"]
+
+
+def test_aql_kernarg_layout_matches_code_object():
+    """Every k_safe_step instantiation the AQL path can dispatch takes exactly
+    the argument block csrc/rcbf_aql.hip writes (SafeStepArgs): 16 8-B
+    scalars / pointers, auto_reset, seed, env_offset, the 240-B rcbf_params by
+    value, prior_cols, the stamp pointer -- no hidden arguments -- and uses no
+    scratch (checked again against the loaded symbols by rcbf_aql_open)."""
+    from rcbf_amd import _lib
+    want = [(8 * i, 8) for i in range(16)] + [(128, 4), (136, 8), (144, 8), (152, ctypes.sizeof(_lib.RcbfParams)),
+                                              (392, 4), (400, 8)]
+    ks = [k for k in _steps_code_object_kernels() if k[".name"].startswith("_ZN4rcbf11k_safe_step")]
+    # solver x mode/hazards x workgroup size x (product, span)
+    assert len(ks) >= 3 * 9 * 2
+    for k in ks:
+        assert k[".kernarg_segment_size"] == 408, k[".name"]
+        assert [(a[".offset"], a[".size"]) for a in k[".args"]] == want, k[".name"]
+        assert all(not a[".value_kind"].startswith("hidden") for a in k[".args"]), k[".name"]
+        assert k[".private_segment_fixed_size"] == 0, k[".name"]
+
+
+def test_aql_entry_points_reject_bad_arguments_without_gpu():
+    from rcbf_amd import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.rcbf_aql_open(0, None, 0, None) == 1003
+    assert lib.rcbf_aql_open(-1, None, 0, ctypes.byref(h)) == 1002  # no such HIP device (none here)
+    assert lib.rcbf_aql_run(None, 0) == 1003
+    assert lib.rcbf_aql_plan_free(None) == 0
+    assert lib.rcbf_aql_close(None) == 0

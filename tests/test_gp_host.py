@@ -258,3 +258,197 @@ def test_seed_and_load_none():
     assert dm.disturb_estimators is None
     with pytest.raises(Exception, match="Could not load GP models from /nonexistent"):
         dm.load_disturbance_models("/nonexistent")
+
+
+# -- gpytorch's eval-mode mean solve --------------------
+def _kernel_only(rng, N, D, ls=1.4, os_=0.3):
+    x = rng.normal(0, 1, (N, D))
+    d2 = ((x[:, None] - x[None]) ** 2).sum(-1)
+    return os_ * np.exp(-0.5 * d2 / ls ** 2)
+
+
+def test_pivoted_cholesky_restatements_agree_and_stop():
+    """rcbf_amd.gp.pivoted_cholesky (torch) equals oracle.pivoted_cholesky;
+    both take rank 15 on a full-rank RBF matrix, stop after ONE step on a
+    constant (rank-one) matrix -- the reference's own regime, lengthscale ~1e5
+    -- and L L^T matches K on the pivots."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(1)
+    K = _kernel_only(rng, 600, 4)
+    Lo = O.pivoted_cholesky(K, 15)
+    Lt = gp.pivoted_cholesky(torch.as_tensor(K), 15).numpy()
+    assert Lo.shape == (600, 15) and np.allclose(Lt, Lo, rtol=0, atol=1e-12)
+    K1 = np.full((500, 500), 0.2) + 1e-12 * _kernel_only(rng, 500, 2)
+    assert O.pivoted_cholesky(K1, 15).shape[1] == 1 and gp.pivoted_cholesky(torch.as_tensor(K1), 15).shape[1] == 1
+    # the error the loop watches: the remaining diagonal after 15 steps is K's diagonal minus diag(L L^T)
+    assert np.all(np.diag(K) - (Lo ** 2).sum(1) >= -1e-12)
+
+
+@pytest.mark.parametrize("N", [700, 1200, 2100])
+def test_cg_mean_solve_matches_oracle(N):
+    """gp.cg_mean_solve (torch, what the fit runs) against oracle.gp_mean_solve
+    (numpy), fp64: the same branch (Cholesky <= 800 points, CG above,
+    preconditioned from 2000), the same iterate to 1e-6 unpreconditioned and
+    1e-3 preconditioned (CG amplifies the two libraries' different rounding);
+    each CG result meets
+    linear_cg's stopping rule -- relative residual below 0.01 after at least 11
+    iterations -- and is NOT the exact solve (it stops early)."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(N)
+    K = _kernel_only(rng, N, 6, ls=1.6, os_=0.4)
+    nz = 0.03
+    y = rng.normal(0, 1, N)
+    xo, its = O.gp_mean_solve(K, nz, y, return_iters=True)
+    xt = gp.cg_mean_solve(torch.as_tensor(K), nz, torch.as_tensor(y)).numpy()
+    # the preconditioned iteration's residual norm is not monotone and the two libraries' rounding drifts apart
+    # over ~55 iterations (either result meets the stopping rule; tests below check both)
+    bar = 1e-6 if N < 2000 else 1e-3
+    assert np.max(np.abs(xt - xo)) <= bar * np.max(np.abs(xo))
+    C = K + nz * np.eye(N)
+    if N > 800:
+        assert np.linalg.norm(C @ xt - y) < O.CG_EVAL_TOLERANCE * np.linalg.norm(y)
+    exact = np.linalg.solve(C, y)
+    if N <= 800:
+        assert its == 0 and np.max(np.abs(xo - exact)) <= 1e-9 * np.max(np.abs(exact))
+    else:
+        assert its >= 11
+        assert np.linalg.norm(C @ xo - y) < O.CG_EVAL_TOLERANCE * np.linalg.norm(y)
+        assert np.max(np.abs(xo - exact)) > 1e-8 * np.max(np.abs(exact))
+
+
+def test_cg_preconditioner_is_the_woodbury_inverse():
+    """The preconditioner of linear_operator's AddedDiagLinearOperator, v ->
+    (v - Q Q^T v) / n with [L; sqrt(n) I] = Q R, is (L L^T + n I)^-1 v."""
+    rng = np.random.default_rng(8)
+    K = _kernel_only(rng, 300, 3)
+    nz = 0.05
+    L = O.pivoted_cholesky(K, 15)
+    k = L.shape[1]
+    Q, _ = np.linalg.qr(np.concatenate([L, np.sqrt(nz) * np.eye(k)], 0))
+    Q = Q[:300]
+    v = rng.normal(0, 1, 300)
+    got = (v - Q @ (Q.T @ v)) / nz
+    want = np.linalg.solve(L @ L.T + nz * np.eye(300), v)
+    assert np.max(np.abs(got - want)) <= 1e-9 * np.max(np.abs(want))
+
+
+def test_gp_model_mean_solve_setting():
+    """GPDisturbanceModel(mean_solve="cg") puts gpytorch's eval-mode alpha in
+    the mean column of the device factor; DynamicsModel takes it by default
+    and "exact" on request."""
+    from rcbf_amd import gp
+    from rcbf_amd.dynamics import DynamicsModel
+    rng = np.random.default_rng(2)
+    tx, ty = _data(rng, 900, 3)
+    hyper = [(1.3, 0.3, 0.02), (1.1, 0.2, 0.05), (2.0, 0.4, 0.03)]
+    m = gp.GPDisturbanceModel(tx, ty, hyper, device="cpu", mean_solve="cg")
+    q = rng.normal(0, 1, (40, 3)) * tx.std(0)
+    # the model's alpha is the restated CG iterate (to the CG cross-library bar); the mean column carries it
+    xn = (tx / (tx.std(0) + 1e-8)).astype(np.float32).astype(np.float64)
+    yn = (ty / (ty.std(0) + 1e-8)).astype(np.float32).astype(np.float64)
+    d2x = ((xn[:, None, :] - xn[None]) ** 2).sum(-1)
+    for i, (ls, os_, nz) in enumerate(hyper):
+        ao = O.gp_mean_solve(os_ * np.exp(-0.5 * d2x / ls ** 2), nz, yn[:, i])
+        # 1e-4: the kernel matrices differ in the last bits (cdist vs explicit differences) and CG amplifies it
+        assert np.max(np.abs(m.alpha[i].numpy() - ao)) <= 1e-4 * np.max(np.abs(ao))
+    mo, _ = O.gp_predict(q, tx, ty, hyper, alpha=m.alpha.numpy())
+    me, _ = O.gp_predict(q, tx, ty, hyper)
+    xq = (q / tx.std(0)).astype(np.float32).astype(np.float64)
+    Rt = m.logical_Rt().double().numpy()
+    for i in range(3):
+        xs = xq * float(m.inv_sl[i])
+        xt = m.xt[i].double().numpy()
+        d2 = np.maximum((xs * xs).sum(1)[:, None] + m.tn2[i].double().numpy()[None] - 2 * xs @ xt.T, 0.0)
+        mean = (float(m.outscale[i]) * np.exp(-d2)) @ Rt[i][:, m.r] * float(m.y_scale[i])
+        # 2e-4: the GPU suite's mean bar (alpha is stored in fp32 and the mean is a cancelling sum)
+        assert np.max(np.abs(mean - mo[:, i])) <= 2e-4 * np.max(np.abs(mo[:, i]))
+    assert np.max(np.abs(mo - me)) > 1e-6 * np.max(np.abs(me))  # the CG mean is not the exact one
+    env = types.SimpleNamespace(dynamics_mode="Unicycle", dt=0.02)
+    assert DynamicsModel(env, types.SimpleNamespace(cuda=False)).gp_mean == "cg"
+    assert DynamicsModel(env, types.SimpleNamespace(cuda=False, gp_mean="exact")).gp_mean == "exact"
+    with pytest.raises(ValueError):
+        gp.GPDisturbanceModel(tx, ty, hyper, device="cpu", mean_solve="pcg")
+
+
+def test_love_start_vectors_leave_the_global_rng_alone():
+    """the Lanczos start vectors come from a generator of their
+    own, so a fit does not advance torch's global CPU stream."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(6)
+    tx, ty = _data(rng, 120, 3)
+    hyper = [(1.3, 0.3, 0.02)] * 3
+    torch.manual_seed(11)
+    before = torch.get_rng_state()
+    g = torch.Generator()
+    g.manual_seed(5)
+    a = gp.GPDisturbanceModel(tx, ty, hyper, device="cpu", rank=20, love_generator=g)
+    assert torch.equal(torch.get_rng_state(), before)
+    g.manual_seed(5)
+    b = gp.GPDisturbanceModel(tx, ty, hyper, device="cpu", rank=20, love_generator=g)
+    assert torch.equal(a.love_init, b.love_init)
+
+
+def _reference_state_dict(raw_noise, raw_os, raw_ls, bounds=True):
+    """A state_dict with the keys and shapes gpytorch gives the reference's
+    BaseGPy (ZeroMean, ScaleKernel(RBFKernel) with NormalPriors,
+    GaussianLikelihood); values synthetic."""
+    from collections import OrderedDict
+    sd = OrderedDict()
+    sd["likelihood.noise_covar.raw_noise"] = torch.tensor([raw_noise])
+    if bounds:
+        sd["likelihood.noise_covar.raw_noise_constraint.lower_bound"] = torch.tensor(1e-4)
+        sd["likelihood.noise_covar.raw_noise_constraint.upper_bound"] = torch.tensor(float("inf"))
+    sd["covar_module.raw_outputscale"] = torch.tensor(raw_os)
+    sd["covar_module.base_kernel.raw_lengthscale"] = torch.tensor([[raw_ls]])
+    sd["covar_module.base_kernel.lengthscale_prior.loc"] = torch.tensor(1e5)
+    sd["covar_module.base_kernel.lengthscale_prior.scale"] = torch.tensor(1e-5)
+    if bounds:
+        sd["covar_module.base_kernel.raw_lengthscale_constraint.lower_bound"] = torch.tensor(0.0)
+        sd["covar_module.raw_outputscale_constraint.lower_bound"] = torch.tensor(0.0)
+    sd["covar_module.outputscale_prior.loc"] = torch.tensor(0.2)
+    sd["covar_module.outputscale_prior.scale"] = torch.tensor(1e-5)
+    return sd
+
+
+@pytest.mark.parametrize("bounds", [True, False])
+def test_load_reference_format_checkpoint(tmp_path, bounds):
+    """load_disturbance_models reads what the REFERENCE's
+    save_disturbance_models writes (dynamics.py:408-419: a list of gpytorch
+    state_dicts, the training data as numpy arrays), through the weights-only
+    unpickler, mapping raw parameters through gpytorch's constraints
+    (softplus + lower bound; the noise's 1e-4 when the bound is not stored).
+    The GPs condition on the raw training data, as the reference rebuilds
+    them (:401-403).  Parity unpinned: the state_dicts are synthetic."""
+    from rcbf_amd.dynamics import DynamicsModel
+    rng = np.random.default_rng(3)
+    tx, ty = _data(rng, 150, 3)
+    raws = [(-2.0, -1.4, 11.5), (0.3, -1.5, 11.51), (-5.0, -1.3, 11.49)]
+    torch.save([_reference_state_dict(*r, bounds=bounds) for r in raws], tmp_path / "gp_models.pkl")
+    torch.save(tx, tmp_path / "gp_models_train_x.pkl")  # numpy arrays, as the reference saves them
+    torch.save(ty, tmp_path / "gp_models_train_y.pkl")
+    env = types.SimpleNamespace(dynamics_mode="Unicycle", dt=0.02)
+    dm = DynamicsModel(env, types.SimpleNamespace(cuda=False))
+    dm.load_disturbance_models(str(tmp_path))
+    sp = lambda v: float(np.log1p(np.exp(np.float64(np.float32(v)))))  # noqa: E731  (the raw values are fp32)
+    want = [(sp(ls), sp(os_), sp(nz) + 1e-4) for nz, os_, ls in raws]
+    assert np.allclose(np.array(dm.disturb_estimators.hyper), np.array(want), rtol=1e-7, atol=0)  # fp32 bounds
+    assert dm.disturb_estimators.raw_train and np.array_equal(dm.train_x, tx)
+    # the device factor conditions on the raw data: against the oracle with raw_train
+    m = dm.disturb_estimators
+    q = rng.normal(0, 1, (20, 3)) * tx.std(0)
+    mo, _ = O.gp_predict(q, tx, ty, want, raw_train=True, alpha=m.alpha.numpy())
+    xq = (q / tx.std(0)).astype(np.float32).astype(np.float64)
+    Rt = m.logical_Rt().double().numpy()
+    for i in range(3):
+        xs = xq * float(m.inv_sl[i])
+        xt = m.xt[i].double().numpy()
+        d2 = np.maximum((xs * xs).sum(1)[:, None] + m.tn2[i].double().numpy()[None] - 2 * xs @ xt.T, 0.0)
+        mean = (float(m.outscale[i]) * np.exp(-d2)) @ Rt[i][:, m.r] * float(m.y_scale[i])
+        assert np.max(np.abs(mean - mo[:, i])) <= 1e-4 * np.max(np.abs(mo[:, i])) + 1e-9
+    # and our own format keeps the flag across a save / load
+    dm.save_disturbance_models(str(tmp_path / ".."))
+    dm2 = DynamicsModel(env, types.SimpleNamespace(cuda=False))
+    dm2.load_disturbance_models(str(tmp_path / ".."))
+    assert dm2.disturb_estimators.raw_train and dm2.disturb_estimators.hyper == dm.disturb_estimators.hyper
+    with pytest.raises(Exception, match="Could not load GP models"):
+        dm2.load_disturbance_models(str(tmp_path / "missing"))

@@ -100,7 +100,11 @@ def test_dynamics_model_love_fit_and_predict():
     assert gpm.rank == 100 and gpm.love_init is not None and gpm.r <= 100
     qs = rng.normal(0, 1, (257, 3)).astype(np.float32)
     mean, std = dm.predict_disturbance(torch.as_tensor(qs, device="cuda"))
-    mo, so = O.gp_predict(qs, dm.train_x, dm.train_y, gpm.hyper, rank=100, love_init=gpm.love_init.numpy())
+    # the mean weights are gpytorch's eval-mode CG iterate (DynamicsModel's default, checked against the
+    # oracle's restatement on the CPU in tests/test_gp_host.py): the posterior kernels are checked on them
+    assert dm.gp_mean == "cg" and gpm.mean_solve == "cg"
+    mo, so = O.gp_predict(qs, dm.train_x, dm.train_y, gpm.hyper, rank=100, love_init=gpm.love_init.numpy(),
+                          alpha=gpm.alpha.cpu().numpy())
     _check(mean.cpu().numpy(), std.cpu().numpy(), mo, so)
 
 
@@ -291,6 +295,7 @@ def test_gp_gemv_handoff_across_calls(rank):
     qd = torch.as_tensor(q, device="cuda")
     offs = np.concatenate([[0], np.cumsum(sizes)])
     model.predict(qd[:8].contiguous())  # size the workspace for B = 8 before the capture
+    ws = model._workspace(8)[0]
     xs = [qd[offs[j]:offs[j + 1]].clone() for j in range(48)]
     outs = [(torch.empty(sizes[j], 10, device="cuda"), torch.empty(sizes[j], 10, device="cuda")) for j in range(48)]
     import ctypes
@@ -301,7 +306,7 @@ def test_gp_gemv_handoff_across_calls(rank):
     with torch.cuda.graph(g, stream=s):
         for j in range(48):
             rc = lib.rcbf_gp_predict(ctypes.byref(model._m), sizes[j], _lib.ptr(xs[j]), _lib.ptr(outs[j][0]),
-                                     _lib.ptr(outs[j][1]), _lib.ptr(model._ws), _lib.stream_of(torch.device("cuda")))
+                                     _lib.ptr(outs[j][1]), _lib.ptr(ws), _lib.stream_of(torch.device("cuda")))
             assert rc == 0
     mo, so = O.gp_predict(q, tx, ty, hyper, rank=rank, love_init=None if rank is None else model.love_init.numpy())
     side = torch.cuda.Stream()
@@ -319,9 +324,39 @@ def test_gp_gemv_handoff_across_calls(rank):
         torch.cuda.synchronize()
         for j in range(48):
             _check(outs[j][0].cpu().numpy(), outs[j][1].cpu().numpy(), mo[offs[j]:offs[j + 1]], so[offs[j]:offs[j + 1]])
-    # the arrival counters (one per 128-B line: n_s (n_cb + 1) of them) lead the workspace and are zero again
-    n_ctr = model.n_s * (model._m.C_pad // 128 + 1) * 32
-    assert int(model._ws.view(torch.int32)[:n_ctr].abs().sum()) == 0
+    # the arrival counters (one per 128-B line: n_s (n_cb + 1) of them) and the fail word's line lead the
+    # workspace and are zero again
+    n_ctr = model.n_s * (model._m.C_pad // 128 + 1) * 32 + 32
+    assert int(ws.view(torch.int32)[:n_ctr].abs().sum()) == 0
+    model.check_failures()
+
+
+@pytest.mark.parametrize("rank", [100, None])
+def test_gp_gemv_poisoned_counter_is_detected_and_reset(rank):
+    """a GEMV call that finds a non-zero arrival counter
+    (a workspace not zero-filled, an aborted call, two calls sharing one
+    workspace) sets the workspace's fail word; check_failures
+    (rcbf_gp_workspace_check) raises and zeroes the counters, and the next
+    call is correct again (bit-equal to the clean call before the poison)."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(5 + (rank or 0))
+    tx, ty = _data(rng, 1500, 10)
+    hyper = [(rng.uniform(0.8, 2.5), rng.uniform(0.05, 0.5), rng.uniform(0.01, 0.2)) for _ in range(10)]
+    model = gp.GPDisturbanceModel(tx, ty, hyper, rank=rank)
+    q = torch.as_tensor((rng.normal(0, 1, (1, 10)) * tx.std(0)).astype(np.float32), device="cuda")
+    m1, s1 = model.predict(q)
+    model.check_failures()
+    ws = model._workspace(1)[0]
+    n_cb = model._m.C_pad // 128
+    # GP 0's first block counter; GP 3's counter (used only by a multi-block factor: the exact posterior)
+    for word in [0] + ([(model.n_s * n_cb + 3) * 32] if n_cb > 1 else []):
+        ws.view(torch.int32)[word] = 5
+        model.predict(q)
+        with pytest.raises(RuntimeError, match="arrival counter"):
+            model.check_failures()
+        m2, s2 = model.predict(q)
+        model.check_failures()
+        assert torch.equal(m1, m2) and torch.equal(s1, s2)
 
 
 def test_state_from_obs_kernel_matches_reference_get_state(golden):

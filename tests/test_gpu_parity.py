@@ -347,6 +347,40 @@ def test_cascade_config_size_golden(golden):
     assert us.shape == (4096, 2) and rel(us, c["uni3_usafe"]) <= 1e-7
 
 
+def test_cascade_slack_and_violation_warning(golden, capsys):
+    """get_u_safe returns the QP's slack epsilon
+    (rcbf_cascade_u_safe eps_out) and prints the reference's warning for every
+    row with |epsilon| > 0.1 (cbf_qp.py:283-284).  The slack is checked
+    against the exact QP on the normalised fp64 rows (oracle), on the 4096
+    config-size cars rows plus unicycle states placed inside a hazard (which
+    need a large slack)."""
+    from rcbf_amd.cbf_qp import CascadeCBFLayer
+    from rcbf_amd.envs import SimulatedCarsEnv, UnicycleEnv
+    c = golden("cascade_config")
+    cl = CascadeCBFLayer(SimulatedCarsEnv(), gamma_b=20.0, k_d=3.0)
+    env = UnicycleEnv()
+    ul = CascadeCBFLayer(env, gamma_b=40.0, k_d=3.0, l_p=0.03)
+    rng = np.random.default_rng(3)
+    hz = np.asarray(env.hazards_locations)
+    ux = np.concatenate([hz[:, :2] + rng.normal(0, 0.05, hz.shape), rng.uniform(-np.pi, np.pi, (len(hz), 1))], 1)
+    ux = np.concatenate([ux, np.stack([rng.uniform(-3, 3, 64), rng.uniform(-3, 3, 64),
+                                       rng.uniform(-np.pi, np.pi, 64)], 1)], 0)
+    uu = rng.uniform(-1, 1, (len(ux), 2))
+    um, us_ = np.zeros_like(ux), np.full_like(ux, 0.2)
+    for layer, args in ((cl, (c["cars_u"], c["cars_x"], c["cars_mu"], c["cars_sigma"])), (ul, (uu, ux, um, us_))):
+        capsys.readouterr()
+        layer.get_u_safe(*args)
+        printed = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("CBF indicates")]
+        eps = layer.last_eps
+        P, q, G, h = layer.get_cbf_qp_constraints(*args)
+        Gn, hn, _ = O.normalize_rows(G, h)
+        z, _, _, st = O.qp_exact_general(P, q, Gn, hn)
+        assert (st == 0).all()
+        assert np.max(np.abs(eps - z[:, -1]) / np.maximum(1.0, np.abs(z[:, -1]))) <= 1e-7
+        assert len(printed) == int((np.abs(eps) > 0.1).sum())
+    assert len(printed) >= 1  # the states inside a hazard need the slack
+
+
 def test_cascade_solve_qp_golden(golden):
     """CascadeCBFLayer.solve_qp (cbf_qp.py:242-286) on the reference's own
     rows: the exact fp64 solution (quadprog's), the caller's G normalised in
