@@ -76,10 +76,11 @@ def parse():
                          "all_gather and MAX all_reduce then run on the device (world size 1)")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="CPU/gloo plumbing check of the launcher (no kernel, no measurement)")
-    ap.add_argument("--launch", default="graph", choices=["graph", "seq", "aql"],
-                    help="graph: hipGraph replays of --graph-steps fused steps; seq: the K launches issued from "
-                         "one host call (rcbf_safe_step_seq); aql: the K dispatches as pre-built AQL packets on the "
-                         "library's own HSA queue (rcbf_aql_run, csrc/rcbf_aql.hip), one doorbell per run")
+    ap.add_argument("--launch", default=None, choices=["graph", "seq", "aql"],
+                    help="aql (the default for the fused step): the K dispatches as pre-built AQL packets on the "
+                         "library's own HSA queue (rcbf_aql_run, csrc/rcbf_aql.hip), one doorbell per run; graph "
+                         "(the default for --workload sac_update): hipGraph replays of --graph-steps launches; seq: "
+                         "the K launches issued from one host call (rcbf_safe_step_seq)")
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="(internal) print the CPU baselines as JSON and exit; never touches the GPU")
     ap.add_argument("--host-cores", type=int, default=4,
@@ -92,6 +93,9 @@ def parse():
                     help="step: the fused safe step; sac_update: RCBF_SAC.get_safe_action on a replay batch "
                          "forward + backward (rcbf_obs_safe_action + its backward, config 5)")
     ap.add_argument("--no-span", action="store_true", help="skip the untimed in-kernel span measurement")
+    ap.add_argument("--record", default=None,
+                    help="write this run's roofline evidence (per-step GPU time, dispatch timestamps, span stamps, "
+                         "shader clock) to this JSON file (committed under profiles/ as roofline_record_*.json)")
     ap.add_argument("--prior-values", default="posterior", choices=["posterior", "maxstd"],
                     help="values of the per-env mean/sigma tensors (--prior rows/tensor): posterior = a fitted GP's "
                          "stand-in (small mean, sigma near MAX_STD); maxstd = mean 0, sigma = MAX_STD materialised per "
@@ -109,6 +113,8 @@ def parse():
                       prior_values="maxstd")}.get(args.config, {})
     for k, v in preset.items():
         setattr(args, k, v)
+    if args.launch is None:
+        args.launch = "graph" if (args.workload == "sac_update" or args.no_graph) else "aql"
     if args.workload == "sac_update" and (args.prior == "tensor" or args.launch != "graph" or args.no_graph):
         raise SystemExit("--workload sac_update reads (B, n_s) rows or the in-kernel prior, hipGraph-launched")
     return args
@@ -123,24 +129,38 @@ def aql_dispatch_times(env, layer, ctx, graph, S):
     each dispatch's start / end comes from the packet processor's own
     timestamps (hsa_amd_profiling_get_dispatch_time, the source rocprofv3's
     kernel trace reads).  Returns the per-dispatch durations and the period."""
-    prof = graph.queue.safe_step_plan(env, ctx["pool"], layer, steps=S, mean=ctx["mean"], sigma=ctx["sigma"],
-                                      outputs=ctx["outs"], prior_layout=ctx["layout"], profile=True)
+    from rcbf_amd.aql import PROFILE_ENDS
+    kw = dict(steps=S, mean=ctx["mean"], sigma=ctx["sigma"], outputs=ctx["outs"], prior_layout=ctx["layout"])
+    # end to end: timestamps on the first and the last dispatch only (a signal on every dispatch adds its
+    # own cost to each step), three runs, the median
+    ends = graph.queue.safe_step_plan(env, ctx["pool"], layer, fence_flags=PROFILE_ENDS, **kw)
+    ends.run(sync_hip=True)
+    runs = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ends.run(sync_hip=False)
+        wall = time.perf_counter() - t0
+        t = ends.times_ns().astype(np.float64)
+        runs.append({"first_start_ns": int(t[0, 0]), "last_end_ns": int(t[-1, 1]), "wall_us": round(wall * 1e6, 2),
+                     "period_us": round(float((t[-1, 1] - t[0, 0]) / 1e3 / S), 4)})
+    ends.free()
+    # per dispatch: a completion signal on every dispatch (each one's own duration, with the signal's cost)
+    prof = graph.queue.safe_step_plan(env, ctx["pool"], layer, profile=True, **kw)
     prof.run(sync_hip=True)
-    t0 = time.perf_counter()
-    prof.run(sync_hip=False)
-    wall = time.perf_counter() - t0
     t = prof.times_ns().astype(np.float64)
     prof.free()
     dur = (t[:, 1] - t[:, 0]) / 1e3
     env.check_failures()
-    return {"dispatch_us_mean": round(float(dur.mean()), 4), "dispatch_us_median": round(float(np.median(dur)), 4),
-            "dispatch_us_p10_p90": [round(float(np.percentile(dur, 10)), 4), round(float(np.percentile(dur, 90)), 4)],
-            "period_us": round(float((t[-1, 1] - t[0, 0]) / 1e3 / S), 4),
-            "first_start_to_last_end_us": round(float((t[-1, 1] - t[0, 0]) / 1e3), 3),
-            "profiled_run_wall_us_per_step": round(wall * 1e6 / S, 4), "dispatches": S,
-            "how": "the timed plan's S dispatches re-run with a completion signal each on the same AQL queue "
-                   "(profiling enabled); start / end = the packet processor's dispatch timestamps "
-                   "(hsa_amd_profiling_get_dispatch_time), HSA system clock"}
+    period = float(np.median([r["period_us"] for r in runs]))
+    return {"period_us": round(period, 4), "runs": runs,
+            "signalled_dispatch_us_mean": round(float(dur.mean()), 4),
+            "signalled_dispatch_us_median": round(float(np.median(dur)), 4), "dispatches": S,
+            "how": "the timed plan's S dispatches re-run on the same AQL queue, untimed: period_us = (last dispatch "
+                   "end - first dispatch start) / S from the packet processor's timestamps "
+                   "(hsa_amd_profiling_get_dispatch_time) with a completion signal on the first and last dispatch "
+                   "only, median of 3 runs; signalled_dispatch_us_* = each dispatch's own start-to-end with a "
+                   "signal on every dispatch (the per-dispatch signal adds ~1.5 us, as rocprofv3's tracer does)"}
 
 
 def largest_divisor_le(n, cap):
@@ -469,22 +489,33 @@ def pmc_traffic_file(short, B):
 DRIVER_FORM = (20, 5)  # the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 
 
+DEFAULT_FORM = (1000, 20)  # bench.py with no flags
+
+
 def rocprof_form(steps, warmup):
-    """Which committed trace is "the same command": the driver's 20-step form
-    (kernel_stats_driver_form_<workload>_B<B>_<tag>.csv, rocprofv3 of
-    `bench.py --steps 20 --warmup 5`) or the default long form
-    (kernel_stats_<workload>_B<B>_<tag>.csv, `bench.py` with --steps 1000)."""
-    return "driver" if (steps, warmup) == DRIVER_FORM else "default"
+    """Which committed traces / records are "the same command": the driver's
+    20-step form (rocprofv3 of `bench.py --steps 20 --warmup 5`), the default
+    form (`bench.py`, 1000 steps, 20 warm-up), or None for any other
+    (steps, warmup) -- no committed file is evidence for those."""
+    return {DRIVER_FORM: "driver", DEFAULT_FORM: "default"}.get((steps, warmup))
 
 
-def rocprof_kernel_us(short, B, kernels, form="default"):
+def _form_tag(form, launch):
+    """The form part of a profiles/ file name: driver_form_[aql_] / [aql_]."""
+    aql = "aql_" if launch == "aql" else ""
+    return f"driver_form_{aql}" if form == "driver" else aql
+
+
+def rocprof_kernel_us(short, B, kernels, form="default", launch="graph"):
     """Mean duration (us) of one timed step's kernels -- the sum of their
     AverageNs -- from the newest committed rocprofv3 --kernel-trace --stats
-    summary of this workload in the given command form (rocprof_form);
-    (None, None) if there is none.  The driver form falls back to nothing
-    else: a trace of another command is not evidence for its line."""
+    summary of this workload in the given command form and launch path
+    (kernel_stats_<form tag><workload>_B<B>_<tag>.csv); (None, None) if there
+    is none.  A trace of another command is not evidence for the line."""
     import csv
-    pat = f"kernel_stats_driver_form_{short}_B{B}_*.csv" if form == "driver" else f"kernel_stats_{short}_B{B}_*.csv"
+    if form is None:
+        return None, None
+    pat = f"kernel_stats_{_form_tag(form, launch)}{short}_B{B}_*.csv"
     for path in _profiles_newest(pat):
         try:
             rows = list(csv.DictReader(open(path)))
@@ -500,18 +531,48 @@ def rocprof_kernel_us(short, B, kernels, form="default"):
     return None, None
 
 
-def measure_span(env, layer, ctx, dev, B, bps, n=100):
-    """Untimed, after the timed region: the kernel's own span, untraced.  A
-    hipGraph of n launches of rcbf_safe_step_span (the product kernel plus,
-    per wave, the 100 MHz chip clock at its start and after its stores have
-    landed) replayed twice; per launch, span = last wave end - first wave
-    start, period = next launch's first start - this one's, gap = next
-    launch's first start - this launch's last end (the dependent-kernel
-    boundary).  The span graph's own per-step time by HIP events is reported
-    beside it (the two stamps and a drain per wave)."""
+def roofline_record(short, B, form, launch):
+    """The newest committed roofline record of the same command
+    (profiles/r*/roofline_record_<form tag><workload>_B<B>_<tag>.json, written
+    by `bench.py --record`): (per-step kernel us, path) or (None, None)."""
+    if form is None:
+        return None, None
+    for path in _profiles_newest(f"roofline_record_{_form_tag(form, launch)}{short}_B{B}_*.json"):
+        try:
+            r = json.load(open(path))
+            return float(r["kernel_us_per_step"]), os.path.relpath(path, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
+def measure_span(env, layer, ctx, dev, B, bps, n=100, queue=None):
+    """Untimed, after the timed region: the kernel's own span, untraced.  n
+    launches of rcbf_safe_step_span (the product kernel plus, per wave, the
+    100 MHz chip clock and the shader clock at its start and after its stores
+    have landed) -- a hipGraph replayed twice, or with `queue` (--launch aql)
+    one AQL plan of n dispatches run twice; per launch, span = last wave end -
+    first wave start, period = next launch's first start - this one's, gap =
+    next launch's first start - this launch's last end (the dependent-kernel
+    boundary).  The span run's own per-step time is reported beside it (the
+    stamps and a drain per wave)."""
     nw = (B + 63) // 64
-    buf = torch.zeros(n, nw, 2, dtype=torch.int64, device=dev)
+    buf = torch.zeros(n, nw, 4, dtype=torch.int64, device=dev)
     pool, mean, sigma, layout, outs = ctx["pool"], ctx["mean"], ctx["sigma"], ctx["layout"], ctx["outs"]
+    if queue is not None:
+        from rcbf_amd.aql import PROFILE_ENDS
+        plan = queue.safe_step_plan(env, pool, layer, steps=n, mean=mean, sigma=sigma, outputs=outs,
+                                    prior_layout=layout, span=buf, fence_flags=PROFILE_ENDS)
+        plan.run()
+        torch.cuda.synchronize()
+        buf.zero_()
+        torch.cuda.synchronize()
+        plan.run(sync_hip=False)
+        tt = plan.times_ns().astype(np.float64)
+        plan.free()
+        env.check_failures()
+        return _span_summary(buf, (tt[-1, 1] - tt[0, 0]) / 1e3 / n, n, nw, B, bps,
+                             f"one AQL plan of {n} dispatches (rcbf_aql_run)")
 
     def launches():
         for j in range(n):
@@ -534,7 +595,10 @@ def measure_span(env, layer, ctx, dev, B, bps, n=100):
     e1.record()
     torch.cuda.synchronize()
     env.check_failures()
-    ev_us = e0.elapsed_time(e1) * 1e3 / n
+    return _span_summary(buf, e0.elapsed_time(e1) * 1e3 / n, n, nw, B, bps, f"a hipGraph of {n} launches")
+
+
+def _span_summary(buf, per_step_us, n, nw, B, bps, how_run):
     t = buf.cpu().numpy().astype(np.float64)
     valid = t[:, :, 1] > 0
     start = np.where(valid, t[:, :, 0], np.inf).min(1)
@@ -543,16 +607,24 @@ def measure_span(env, layer, ctx, dev, B, bps, n=100):
     period = np.diff(start) * 0.01
     gap = (start[1:] - end[:-1]) * 0.01
     med = float(np.median(span))
+    # the shader clock each wave ran at: delta(s_memtime) / delta(s_memrealtime) x 100 MHz
+    dreal = np.where(valid, t[:, :, 1] - t[:, :, 0], 0)
+    dmem = np.where(valid, t[:, :, 3] - t[:, :, 2], 0)
+    clk = dmem[dreal > 0] / dreal[dreal > 0] * 100.0
     return {"kernel_span_us_median": round(med, 3), "kernel_span_us_mean": round(float(span.mean()), 3),
             "kernel_span_us_p10_p90": [round(float(np.percentile(span, 10)), 3),
                                        round(float(np.percentile(span, 90)), 3)],
             "period_us_median": round(float(np.median(period)), 3),
             "boundary_gap_us_median": round(float(np.median(gap)), 3),
-            "span_build_events_us_per_step": round(ev_us, 3), "launches": n, "waves_per_launch": nw,
+            "span_run_us_per_step": round(per_step_us, 3), "launches": n, "waves_per_launch": nw,
+            "shader_clock_mhz_median": round(float(np.median(clk)), 1) if clk.size else None,
             "frac_span": round(B * bps / (med * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-            "how": "rcbf_safe_step_span in a hipGraph of 100 launches, untraced: per launch the last wave's end "
-                   "(after its stores landed) minus the first wave's start, s_memrealtime (100 MHz chip clock); "
-                   "frac_span = bytes_per_launch / median span"}
+            "_stamps": {"first_start_ticks": start.astype(np.int64).tolist(),
+                        "last_end_ticks": end.astype(np.int64).tolist()},
+            "how": f"rcbf_safe_step_span, {how_run}, untraced: per launch the last wave's end (after its stores "
+                   "landed) minus the first wave's start, s_memrealtime (100 MHz chip clock); frac_span = "
+                   "bytes_per_launch / median span; shader clock = delta(s_memtime) / delta(s_memrealtime) x "
+                   "100 MHz per wave, median"}
 
 
 def main():
@@ -615,13 +687,16 @@ def main():
         untimed += reps * S
     shard.barrier(world)
     sync()
+    # HIP events bracket the HIP launches; the AQL dispatches run on no HIP stream (their per-launch time
+    # comes from the packet processor's timestamps after the region, aql_dispatch_times), so no event there
+    events = not args.cpu_dry_run and args.launch != "aql"
     t0 = time.perf_counter()
-    if not args.cpu_dry_run:
+    if events:
         ev0.record()
     for _ in range(reps):
         graph.replay()
     t_sub = time.perf_counter() - t0
-    if not args.cpu_dry_run:
+    if events:
         ev1.record()
     sync()
     # this rank's K steps end at its own synchronize; the closing barrier only brackets the region (an RCCL
@@ -630,14 +705,14 @@ def main():
     el = time.perf_counter() - t0
     shard.barrier(world)
     # per fused-step launch, HIP events on the launch stream (torch's current stream)
-    kern_ms = ev0.elapsed_time(ev1) / args.steps if not args.cpu_dry_run else 0.0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps if events else 0.0
     env.check_failures()
     aql_times = {}
     if args.launch == "aql" and not args.cpu_dry_run:
         # no HIP stream carries the AQL dispatches: the per-launch duration comes from the packet processor's
         # dispatch timestamps of the same S steps, re-run profiled right after the timed region
         aql_times = aql_dispatch_times(env, layer, ctx, graph, S)
-        kern_ms = aql_times["dispatch_us_mean"] / 1e3
+        kern_ms = aql_times["period_us"] / 1e3
     per_rank_s = shard.gather_over_ranks(el, world, dev)
     el = max(per_rank_s)
     kern_ms = shard.max_over_ranks(kern_ms, world, dev)
@@ -648,10 +723,11 @@ def main():
     traffic, traffic_src = pmc_traffic_file(short, B)
     kernels = dominant_kernels(args, B)
     rp_form = rocprof_form(args.steps, args.warmup)
-    k_us_rp, rp_src = rocprof_kernel_us(short, B, kernels, rp_form)
+    k_us_rp, rp_src = rocprof_kernel_us(short, B, kernels, rp_form, args.launch)
+    k_us_rec, rec_src = roofline_record(short, B, rp_form, args.launch)
     span = {}
     if world == 1 and not args.cpu_dry_run and not args.no_span and args.workload == "step":
-        span = measure_span(env, layer, ctx, dev, B, bps)
+        span = measure_span(env, layer, ctx, dev, B, bps, queue=getattr(graph, "queue", None))
     extra = {}
     if args.extra and rank == 0 and not args.cpu_dry_run and args.workload == "step":
         extra = extra_measurements(env, layer, dev, args)
@@ -708,10 +784,13 @@ def main():
                      "kernel_us_rocprof": k_us_rp,
                      "frac_rocprof": round(B * bps / (k_us_rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if k_us_rp else None,
                      "rocprof_source": rp_src,
-                     "rocprof_form": (f"driver: rocprofv3 of bench.py --steps {DRIVER_FORM[0]} --warmup {DRIVER_FORM[1]}"
-                                      if rp_form == "driver" else "default: rocprofv3 of bench.py --steps 1000"),
-                     "rocprof_same_command": bool(rp_src) and (rp_form == "driver") == ((args.steps, args.warmup)
-                                                                                          == DRIVER_FORM),
+                     "rocprof_form": {"driver": f"driver: rocprofv3 of bench.py --steps {DRIVER_FORM[0]} --warmup "
+                                                f"{DRIVER_FORM[1]} --launch {args.launch}",
+                                      "default": f"default: rocprofv3 of bench.py --launch {args.launch}"}.get(rp_form),
+                     "rocprof_same_command": bool(rp_src),
+                     "frac_wall": round(B * bps / (el / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                     "record": rec_src, "kernel_us_record": k_us_rec,
+                     "frac_record": round(B * bps / (k_us_rec * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if k_us_rec else None,
                      "timing": "achieved = bytes_per_launch / kernel_ms; kernel_ms = HIP events around the timed "
                                "region / steps (includes the graph launch and the inter-kernel gaps); host_submit_ms "
                                "= host time spent in the graph replay calls; kernel_us_rocprof = the AverageNs of "
@@ -727,14 +806,17 @@ def main():
         rec["roofline"]["rocprof_note"] = ("the traced mean exceeds ms_per_step: rocprofv3 --kernel-trace serialises "
                                            "each dispatch with its own completion signal (tracer control: +2.2-2.5 us "
                                            "per dispatch); frac_rocprof is a traced figure, frac the untraced one")
+    stamps = span.pop("_stamps", None) if span else None
     if span:
         rec["roofline"]["span"] = span
     if aql_times:
         rec["roofline"]["aql_dispatch_times"] = aql_times
-        rec["roofline"]["timing"] = ("achieved = bytes_per_launch / kernel_ms; kernel_ms = the mean dispatch duration "
-                                     "(packet processor timestamps) of the timed plan's steps re-run profiled on the "
-                                     "same queue (aql_dispatch_times); host_submit_ms = host time of the timed run "
-                                     "call (submission AND the wait for completion)")
+        rec["roofline"]["timing"] = ("achieved = bytes_per_launch / kernel_ms; kernel_ms = the per-step GPU time of "
+                                     "the timed plan's steps re-run on the same queue, (last dispatch end - first "
+                                     "dispatch start) / steps from the packet processor's timestamps "
+                                     "(aql_dispatch_times.period_us; the AQL counterpart of HIP events around the "
+                                     "region); host_submit_ms = host time of the timed run call (submission AND the "
+                                     "wait for completion)")
     if world > 1:  # the spread of the timed region over ranks (value is set by the slowest)
         ms = sorted(v / args.steps * 1e3 for v in per_rank_s)
         rec["per_rank_ms"] = {"min": round(ms[0], 5), "median": round(float(np.median(ms)), 5),
@@ -745,10 +827,36 @@ def main():
         if host_mask:  # the child starts with every allowed core
             os.sched_setaffinity(0, host_mask)
         rec.update(cpu_baselines_in_child(args))
+    if rank == 0 and args.record and not args.cpu_dry_run:
+        write_record(args, rec, short, B, bps, kern_ms, aql_times, span, stamps)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
+
+
+def write_record(args, rec, short, B, bps, kern_ms, aql_times, span, stamps):
+    """--record PATH: the roofline evidence of this run as one JSON file --
+    the command, the per-step GPU time `frac` is computed from
+    (kernel_us_per_step: AQL first-dispatch-start to last-dispatch-end per step,
+    or HIP events), the raw per-run dispatch timestamps, the per-launch span
+    stamps (first wave start, last wave end, 100 MHz ticks) and the shader
+    clock.  Committed under profiles/ as roofline_record_<form tag><workload>
+    _B<B>_<tag>.json, bench.py reads it back (roofline.record, frac_record)."""
+    out = {"what": "roofline record of one bench.py run (bench.py --record)",
+           "command": "bench.py " + " ".join(a for a in sys.argv[1:] if not a.startswith("--record")
+                                             and a != args.record),
+           "form": rocprof_form(args.steps, args.warmup), "launch": args.launch, "workload": short, "batch": B,
+           "steps": args.steps, "warmup": args.warmup, "bytes_per_env_step": bps, "bytes_per_launch": B * bps,
+           "ms_per_step": rec["ms_per_step"], "kernel_us_per_step": round(kern_ms * 1e3, 4),
+           "peak_GBs": HBM_PEAK_GBS, "frac": rec["roofline"]["frac"], "frac_wall": rec["roofline"]["frac_wall"],
+           "recompute": "frac = bytes_per_launch / (kernel_us_per_step * 1e-6) / 1e9 / peak_GBs; frac_wall the "
+                        "same with ms_per_step; frac_span with span.kernel_span_us_median",
+           "aql_dispatch_times": aql_times or None, "span": span or None, "span_stamps": stamps,
+           "value": rec["value"]}
+    os.makedirs(os.path.dirname(os.path.abspath(args.record)), exist_ok=True)
+    with open(args.record, "w") as f:
+        json.dump(out, f, indent=1)
 
 
 def unicycle_hazards(k):

@@ -279,6 +279,29 @@ int rcbf_gp_workspace_check(const rcbf_gp_model* m, float* workspace, hipStream_
 int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* mean_out,
                     float* std_out, float* workspace, hipStream_t stream);
 
+/* RCBF_SAC.get_safe_action of ONE observation with the fitted GP (sac_cbf.py:
+ * 218-238 as main.py:93 calls it, through select_action, every env step) in
+ * ONE launch: get_state(obs) (dynamics.py:190-232) formed in every workgroup,
+ * the GP posterior of rcbf_gp_predict's B <= 8 GEMV on it (dynamics.py:342-
+ * 390), and, in the last workgroup to finish a GP, the one-launch safe action
+ * on the posterior (diff_cbf_qp.py:44-79: rows, normalisation, exact QP,
+ * clamp) -- the arithmetic of rcbf_state_from_obs -> rcbf_gp_predict ->
+ * rcbf_obs_safe_action, so the action is bit-equal to those three launches.
+ * B must be 1; prm: the layer (solver RCBF_SOLVER_ACTIVE_SET, mode matching
+ * m->n_s).  obs (1, n_o), u_rl (1, n_u) f32 device; mean_out / std_out
+ * [nullable] (1, n_s) the posterior; u_out [nullable] (1, n_u) f32 device;
+ * u_host [nullable] (1, n_u) f32 in pinned host memory (rcbf_host_alloc);
+ * done_word [nullable] a pinned host word: when given, the kernel stores `seq`
+ * into it (system scope) after the action, and the call RETURNS WHEN IT READS
+ * `seq` -- the action is then on the host, with no copy or stream
+ * synchronisation (as rcbf_env_step_sync).  The workspace is the GP's
+ * (rcbf_gp_workspace_floats(m, 1), zero-filled once).  RCBF_E_BAD_MODE for
+ * another solver; RCBF_E_BAD_SHAPE for B != 1 or a model of another width. */
+int rcbf_gp_obs_safe_action(const rcbf_params* prm, const rcbf_gp_model* m, int64_t B, const float* obs,
+                            const float* u_rl, float* mean_out, float* std_out, float* u_out, float* u_host,
+                            uint32_t* done_word, uint32_t seq, int32_t* status_out, int32_t* fail_flag,
+                            float* workspace, hipStream_t stream);
+
 /* rcbf_gp_predict that also (or only) writes the COLUMN layout the fused
  * step reads (rcbf_safe_step_cols): mean_cols / std_cols (n_cols, B) f32 of
  * the output dimensions cols[0..n_cols) (a host array, n_cols <= 10), e.g.
@@ -449,7 +472,9 @@ int rcbf_safe_step_seq_cols(const rcbf_params* prm, int64_t B, int32_t K, double
  * (prior_cols = 1), the same instructions, plus per wavefront w (lanes
  * 64w..64w+63 of the launch, w < ceil(B / 64)) lane 0 writes the 100 MHz chip
  * clock (s_memrealtime) at the wave's start and after its own stores have
- * completed: span_out[2w], span_out[2w+1] (uint64, 16-B aligned).  The
+ * completed: span_out[4w], span_out[4w+1], and the shader clock (s_memtime)
+ * at the same two points: span_out[4w+2], span_out[4w+3] (uint64, 16-B
+ * aligned; delta(memtime) / delta(memrealtime) x 100 MHz = the clock).  The
  * launch's kernel span is max(end) - min(start) over its waves. */
 int rcbf_safe_step_span(const rcbf_params* prm, int64_t B, double* x, double* aux, int32_t* step,
                         uint32_t* episode, const float* u_rl, const float* mu, const float* sigma,
@@ -491,20 +516,25 @@ int rcbf_safe_rollout(const rcbf_params* prm, int64_t B, int32_t K, double* x, d
  * rcbf_aql_safe_step_plan: the arguments of rcbf_safe_step_seq (prior_cols =
  * 1: the column layout of rcbf_safe_step_cols) plus span_out [nullable] (the
  * measurement instantiation of rcbf_safe_step_span; step j writes its stamps
- * to span_out[2 ceil(B/64) j ...], K blocks of rcbf_safe_step_span's layout); the K
+ * to span_out[4 ceil(B/64) j ...], K blocks of rcbf_safe_step_span's layout); the K
  * kernel-argument blocks are copied to device memory here (synchronous), so
  * the buffers must stay allocated while the plan exists.  flags
  * RCBF_AQL_PROFILE: a completion signal per dispatch, read back with
- * rcbf_aql_plan_times (start, end in ns of the HSA system clock per step).
+ * rcbf_aql_plan_times (start, end in ns of the HSA system clock per step);
+ * RCBF_AQL_PROFILE_ENDS: on the first and last dispatch only (the others
+ * read back as 0).
  * rcbf_aql_run: submit the K dispatches (barrier bit on each), ring the
  * doorbell once, busy-wait for completion; timeout_us 0 -> 10 s.
  * Returns RCBF_E_HSA / RCBF_E_TIMEOUT on a queue error or a timeout. */
 #define RCBF_AQL_PROFILE 1
-/* plan flags: memory-fence scopes of the first / last packet (default: system
- * scope at both ends, agent scope between steps) */
-#define RCBF_AQL_FIRST_ACQUIRE_AGENT 2 /* the first step acquires at agent scope */
-#define RCBF_AQL_LAST_RELEASE_AGENT 4  /* the last step releases at agent scope */
-#define RCBF_AQL_STUDY_MID_NOFENCE 8   /* STUDY ONLY: no fences between steps (not coherent across XCDs) */
+/* plan flags: memory-fence scopes (default: agent scope everywhere but the
+ * last packet's release, which is system scope) */
+#define RCBF_AQL_FIRST_ACQUIRE_SYSTEM 2 /* the first step acquires at system scope (inputs in host memory) */
+#define RCBF_AQL_LAST_RELEASE_AGENT 4   /* the last step releases at agent scope */
+#define RCBF_AQL_STUDY_MID_NOFENCE 8    /* STUDY ONLY: no fences between steps (not coherent across XCDs) */
+#define RCBF_AQL_STUDY_MID_NOACQ 16     /* STUDY ONLY: no acquire between steps */
+#define RCBF_AQL_STUDY_MID_NOREL 32     /* STUDY ONLY: no release between steps */
+#define RCBF_AQL_PROFILE_ENDS 64        /* timestamps of the first and the last dispatch only */
 #define RCBF_AQL_SAFE_STEP_KERNARG_BYTES 408 /* sizeof the k_safe_step argument block */
 typedef struct rcbf_aql rcbf_aql;
 typedef struct rcbf_aql_plan rcbf_aql_plan;

@@ -19,11 +19,14 @@
 // host-side cost of K dispatches is ~1 us and the packet processor starts the
 // first kernel as soon as it reads the packet.  Every packet has the barrier
 // bit: step j + 1 starts after step j has completed, exactly like K launches
-// on one in-order stream.  Memory scopes: the first packet acquires at system
-// scope and the last releases at system scope (the host reads the completion
-// signal; HIP work after the call sees the results), the packets between
+// on one in-order stream.  Memory scopes: the last packet releases at system
+// scope (the host reads the completion signal; HIP work after the call sees
+// the results), the packets between
 // acquire and release at agent scope, which on gfx950 writes the XCD L2s back
-// and invalidates them between steps as HIP's in-order stream does.
+// and invalidates them between steps as HIP's in-order stream does.  The first
+// packet acquires at agent scope: every input of the step is device memory
+// written by device work or copies that completed before the run (a system-
+// scope acquire there cost the first step ~3 us: profiles/r06/aql_fences_r06e.json).
 //
 // Reference interface this serves: env.step() of the batched env inside the
 // SAC loop (main.py:93-95, sac_cbf.py:218-238) -- a synchronous call, like a
@@ -332,7 +335,11 @@ int rcbf_aql_safe_step_plan(rcbf_aql* q, const rcbf_params* prm, int64_t B, int3
     if (prior_cols && prm->mode == RCBF_MODE_SIMULATED_CARS && mu) return RCBF_E_BAD_SHAPE;
     if (span_out && (((uintptr_t)span_out) & 15)) return RCBF_E_BAD_SHAPE;
     if (span_out && prm->solver != RCBF_SOLVER_ACTIVE_SET) return RCBF_E_BAD_MODE;
-    const bool profiled = (flags & RCBF_AQL_PROFILE) != 0;
+    // RCBF_AQL_PROFILE: a completion signal (timestamps) on every packet; RCBF_AQL_PROFILE_ENDS: on the first
+    // and the last only, so the run is timed end to end without a signal between steps (each one adds
+    // ~1.5 us to its step: profiles/r06/aql_dispatch_signal_cost)
+    const bool ends = (flags & RCBF_AQL_PROFILE_ENDS) != 0;
+    const bool profiled = (flags & RCBF_AQL_PROFILE) != 0 || ends;
     if (profiled && !q->profiling) return RCBF_E_BAD_MODE;
     DeviceGuard guard(q->device);
     // the launch rcbf_safe_step would make: solver, mode, hazards, workgroup size
@@ -347,7 +354,7 @@ int rcbf_aql_safe_step_plan(rcbf_aql* q, const rcbf_params* prm, int64_t B, int3
     auto* p = new rcbf_aql_plan();
     p->q = q;
     p->K = K;
-    p->profiled = profiled ? 1 : 0;
+    p->profiled = ends ? 2 : profiled ? 1 : 0;
     std::vector<unsigned char> host((size_t)K * kArgStride, 0);
     for (int32_t j = 0; j < K; ++j) {
         SafeStepArgs a;
@@ -373,14 +380,14 @@ int rcbf_aql_safe_step_plan(rcbf_aql* q, const rcbf_params* prm, int64_t B, int3
         a.off = env_offset;
         a.prm = *prm;
         a.prior_cols = prior_cols ? 1 : 0;
-        // step j's stamps: its own block of 2 ceil(B / 64) words
-        a.stamp_buf = span_out ? reinterpret_cast<unsigned long long*>(span_out) + (size_t)j * 2 * ((B + 63) / 64)
+        // step j's stamps: its own block of 4 ceil(B / 64) words
+        a.stamp_buf = span_out ? reinterpret_cast<unsigned long long*>(span_out) + (size_t)j * 4 * ((B + 63) / 64)
                                : nullptr;
         std::memcpy(host.data() + (size_t)j * kArgStride, &a, sizeof a);
     }
     int rc = (int)hipMalloc(&p->kernargs, host.size());
     if (!rc) rc = (int)hipMemcpy(p->kernargs, host.data(), host.size(), hipMemcpyHostToDevice);
-    const int nsig = profiled ? K : 1;
+    const int nsig = p->profiled == 1 ? K : p->profiled == 2 ? 2 : 1;
     for (int j = 0; !rc && j < nsig; ++j) {
         hsa_signal_t s;
         rc = hsa_rc(hsa_signal_create(1, 0, nullptr, &s));
@@ -394,10 +401,10 @@ int rcbf_aql_safe_step_plan(rcbf_aql* q, const rcbf_params* prm, int64_t B, int3
     for (int32_t j = 0; j < K; ++j) {
         hsa_kernel_dispatch_packet_t& d = p->pkt[j];
         std::memset(&d, 0, sizeof d);
-        int acq = j == 0 && !(flags & RCBF_AQL_FIRST_ACQUIRE_AGENT) ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+        int acq = j == 0 && (flags & RCBF_AQL_FIRST_ACQUIRE_SYSTEM) ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
         int rel = j == K - 1 && !(flags & RCBF_AQL_LAST_RELEASE_AGENT) ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
-        if ((flags & RCBF_AQL_STUDY_MID_NOFENCE) && j > 0) acq = HSA_FENCE_SCOPE_NONE;
-        if ((flags & RCBF_AQL_STUDY_MID_NOFENCE) && j < K - 1) rel = HSA_FENCE_SCOPE_NONE;
+        if ((flags & (RCBF_AQL_STUDY_MID_NOFENCE | RCBF_AQL_STUDY_MID_NOACQ)) && j > 0) acq = HSA_FENCE_SCOPE_NONE;
+        if ((flags & (RCBF_AQL_STUDY_MID_NOFENCE | RCBF_AQL_STUDY_MID_NOREL)) && j < K - 1) rel = HSA_FENCE_SCOPE_NONE;
         d.header = (uint16_t)((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                               (1 << HSA_PACKET_HEADER_BARRIER) | (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                               (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
@@ -412,8 +419,10 @@ int rcbf_aql_safe_step_plan(rcbf_aql* q, const rcbf_params* prm, int64_t B, int3
         d.group_segment_size = ki->group_bytes;
         d.kernel_object = ki->object;
         d.kernarg_address = static_cast<unsigned char*>(p->kernargs) + (size_t)j * kArgStride;
-        if (profiled)
+        if (p->profiled == 1)
             d.completion_signal = p->sig[j];
+        else if (p->profiled == 2 && (j == 0 || j == K - 1))
+            d.completion_signal = p->sig[j == 0 ? 0 : 1];
         else if (j == K - 1)
             d.completion_signal = p->sig[0];
         else
@@ -479,7 +488,13 @@ int rcbf_aql_plan_times(const rcbf_aql_plan* p, uint64_t* start_end_ns) {
     if (!freq) return RCBF_E_HSA;
     for (int32_t j = 0; j < p->K; ++j) {
         hsa_amd_profiling_dispatch_time_t t;
-        if (hsa_amd_profiling_get_dispatch_time(p->q->agent, p->sig[j], &t) != HSA_STATUS_SUCCESS) return RCBF_E_HSA;
+        int si = j;
+        if (p->profiled == 2) {  // only the first and the last packets carry a signal
+            start_end_ns[2 * j] = start_end_ns[2 * j + 1] = 0;
+            if (j != 0 && j != p->K - 1) continue;
+            si = j == 0 ? 0 : 1;
+        }
+        if (hsa_amd_profiling_get_dispatch_time(p->q->agent, p->sig[si], &t) != HSA_STATUS_SUCCESS) return RCBF_E_HSA;
         start_end_ns[2 * j] = (uint64_t)((long double)t.start * 1e9L / (long double)freq);
         start_end_ns[2 * j + 1] = (uint64_t)((long double)t.end * 1e9L / (long double)freq);
     }

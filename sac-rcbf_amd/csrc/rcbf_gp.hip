@@ -440,11 +440,29 @@ constexpr int kGvCtrStride = 32;  // words
 __host__ __device__ inline int64_t gp_fail_word(const rcbf_gp_model& m) {
     return (int64_t)m.n_s * (m.C_pad / kGpCols + 1) * kGvCtrStride;
 }
-inline int64_t gp_counter_words(const rcbf_gp_model& m) { return gp_fail_word(m) + kGvCtrStride; }
+// the line after the fail word: the all-GPs arrival counter of the fused safe action (k_gp_gemv_sa)
+__host__ __device__ inline int64_t gp_sa_word(const rcbf_gp_model& m) { return gp_fail_word(m) + kGvCtrStride; }
+inline int64_t gp_counter_words(const rcbf_gp_model& m) { return gp_fail_word(m) + 2 * kGvCtrStride; }
 
 struct GpCols {
     int32_t n;
     int32_t idx[10];
+};
+
+// The fused RCBF_SAC.get_safe_action of one observation with the GP posterior
+// (k_gp_gemv_sa): what the last workgroup to finish reads and writes.
+struct GpSafeAction {
+    rcbf_params prm;
+    const float* obs;      // (B, n_o) f32 observation rows: the GP query is get_state(obs)
+    const float* u_rl;     // (B, n_u) f32 policy actions
+    float* hmean;          // workspace hand-off of the posterior: (n_s, BQ) mean, std (sc1)
+    float* hstd;
+    float* u_out;          // [nullable] (B, n_u) f32 device
+    float* u_host;         // [nullable] (B, n_u) f32 pinned host memory
+    uint32_t* done_word;   // [nullable] pinned host completion word
+    int32_t* status_out;   // [nullable]
+    int32_t* fail_flag;    // [nullable]
+    uint32_t seq;
 };
 
 // the hand-off's loads and 4-B stores: relaxed agent-scope atomics lower to global_load/store ... sc1
@@ -477,13 +495,18 @@ __device__ __forceinline__ float sum_sc1(const float* p, int n, int64_t stride) 
 // (os, nz, ys: GP i's outputscale, noise and y_scale, loaded at the kernel's start, off the tail)
 __device__ __forceinline__ void gp_gv_finish(const rcbf_gp_model& m, int64_t B, int i, int b, float q, float mraw,
                                              float os, float nz, float ys, float* mean_out, float* std_out,
-                                             const GpCols& cols, float* mean_cols, float* std_cols) {
+                                             const GpCols& cols, float* mean_cols, float* std_cols,
+                                             float* hmean = nullptr, float* hstd = nullptr, int bq = 1) {
     const float lat = fmaxf(os - q, 0.0f);  // latent posterior variance
     const float var = lat + nz;             // likelihood(model(x)).variance
     const float mu = mraw * ys;
     const float sd = sqrtf(var) * ys;
     if (mean_out) mean_out[(int64_t)b * m.n_s + i] = mu;
     if (std_out) std_out[(int64_t)b * m.n_s + i] = sd;
+    if (hmean) {  // the fused safe action's hand-off (write-through, read with sc1 loads)
+        st_sc1(hmean + (int64_t)i * bq + b, mu);
+        st_sc1(hstd + (int64_t)i * bq + b, sd);
+    }
     for (int c = 0; c < cols.n; ++c) {
         if (cols.idx[c] == i) {
             if (mean_cols) mean_cols[(int64_t)c * B + b] = mu;
@@ -492,12 +515,74 @@ __device__ __forceinline__ void gp_gv_finish(const rcbf_gp_model& m, int64_t B, 
     }
 }
 
-template <int D, int BQ>
-__global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
-                                                 int T, unsigned* counters, float* part, float* blk,
-                                                 float* meanraw, float* __restrict__ mean_out,
-                                                 float* __restrict__ std_out, GpCols cols,
-                                                 float* __restrict__ mean_cols, float* __restrict__ std_cols) {
+// The fused safe action's last stage (k_gp_gemv_sa), run by every workgroup that finished a GP: its
+// mean / std went out write-through and drained, then an arrival at the all-GPs counter; the last of the
+// n_s finishers forms RCBF_SAC.get_safe_action for its query rows from the handed-off posterior -- the
+// state from the observation, the CBF rows, the exact QP, the clamp (the arithmetic of
+// rcbf_obs_safe_action, so the result equals the three-launch path bit for bit) -- writes the action to
+// the device and / or pinned host memory, and publishes the completion word system-wide.
+template <int BQ, int SAM, int SAK>
+__device__ __forceinline__ void gp_sa_finish(const rcbf_gp_model& m, int64_t B, unsigned* counters,
+                                             const GpSafeAction& sa) {
+    __shared__ int s_all;
+    const int t = threadIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+        const unsigned tk = ticket(&counters[gp_sa_word(m)]);
+        if (tk >= (unsigned)m.n_s) atomicOr(&counters[gp_fail_word(m)], 1u);
+        s_all = tk == (unsigned)(m.n_s - 1);
+    }
+    __syncthreads();
+    if (!s_all) return;
+    using DD = Dims<SAM, SAK>;
+    if (t < B) {
+        constexpr int NO = Dims<SAM, 1>::NO;
+        float o[NO], xs[DD::NS], us[DD::NU], mm[DD::NS], ss[DD::NS], uf[DD::NU];
+#pragma unroll
+        for (int k = 0; k < DD::NS; ++k) {
+            mm[k] = ld_sc1(sa.hmean + k * BQ + t);
+            ss[k] = ld_sc1(sa.hstd + k * BQ + t);
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) o[k] = sa.obs[(int64_t)t * NO + k];
+#pragma unroll
+        for (int c = 0; c < DD::NU; ++c) us[c] = sa.u_rl[(int64_t)t * DD::NU + c];
+        state_from_obs32<SAM>(o, xs);
+        LayerState<SAM, SAK> L;
+        layer_forward<RCBF_SOLVER_ACTIVE_SET, SAM, SAK>(sa.prm, xs, us, mm, ss, uf, L);
+#pragma unroll
+        for (int c = 0; c < DD::NU; ++c) {
+            if (sa.u_out) sa.u_out[(int64_t)t * DD::NU + c] = uf[c];
+            if (sa.u_host) sa.u_host[(int64_t)t * DD::NU + c] = uf[c];
+        }
+        report(L.qp.status, sa.status_out, t, sa.fail_flag);
+    }
+    __syncthreads();
+    if (t == 0) {
+        atomicExch(&counters[gp_sa_word(m)], 0u);  // consumed: zero for the next call
+        if (sa.done_word) {
+            __threadfence_system();  // the action (and every status word) lands before the word
+            __hip_atomic_store(sa.done_word, sa.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// SAM < 0: the GP posterior alone (k_gp_gemv); SAM = mode, SAK = hazards: the fused safe action
+// (k_gp_gemv_sa, BQ = 1), whose query is get_state(obs) formed in every workgroup.
+template <int D, int BQ, int SAM = -1, int SAK = 1>
+__device__ __forceinline__ void gp_gemv_body(const rcbf_gp_model& m, int64_t B, const float* __restrict__ xq,
+                                             int T, unsigned* counters, float* part, float* blk, float* meanraw,
+                                             float* __restrict__ mean_out, float* __restrict__ std_out,
+                                             const GpCols& cols, float* __restrict__ mean_cols,
+                                             float* __restrict__ std_cols, const GpSafeAction* sa) {
+    constexpr bool kSA = SAM >= 0;
+    float* hmean = nullptr;
+    float* hstd = nullptr;
+    if constexpr (kSA) {
+        hmean = sa->hmean;
+        hstd = sa->hstd;
+    }
     constexpr float kL2E = 1.4426950408889634f;
     constexpr int RJ = kGvRows / 8;  // rows per thread
     __shared__ float s_xs[BQ][D];
@@ -550,7 +635,16 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
     if (t < BQ * D) {
         const int b = t / D, k = t % D;
         const int64_t row = b < B ? b : B - 1;
-        xs_raw = xq[row * D + k];
+        if constexpr (kSA) {  // the query state get_state(obs) (dynamics.py:190-232), as rcbf_state_from_obs forms it
+            constexpr int NO = Dims<(kSA ? SAM : 0), 1>::NO;
+            float o[NO], st[Dims<(kSA ? SAM : 0), 1>::NS];
+#pragma unroll
+            for (int kk = 0; kk < NO; ++kk) o[kk] = sa->obs[row * NO + kk];
+            state_from_obs32<(kSA ? SAM : 0)>(o, st);
+            xs_raw = st[k];
+        } else {
+            xs_raw = xq[row * D + k];
+        }
         xstd = m.x_std[k];
     }
     // 2. the scaled queries (dynamics.py:376: test_x / train_x_std in fp64, then .float()).  The barriers
@@ -686,9 +780,10 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
         if (t < B) {
             const int h = t >> 1, w0 = (t & 1) * 2;
             gp_gv_finish(m, B, i, t, 0.0f + (s_bsum[w0][h] + s_bsum[w0 + 1][h]), s_mean[t], os, nz, ys, mean_out,
-                         std_out, cols, mean_cols, std_cols);
+                         std_out, cols, mean_cols, std_cols, hmean, hstd, BQ);
         }
         if (t == 0) atomicExch(&counters[(i * n_cb + cb) * kGvCtrStride], 0u);
+        if constexpr (kSA) gp_sa_finish<BQ, SAM, SAK>(m, B, counters, *sa);
         return;
     }
     if (t < BQ) {  // query b = t: waves 0, 1 hold even b (slot b / 2), waves 2, 3 odd b
@@ -708,8 +803,32 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
     if (!s_last) return;
     if (t < B)
         gp_gv_finish(m, B, i, t, sum_sc1(blk + (int64_t)i * n_cb * BQ + t, n_cb, BQ),
-                     ld_sc1(meanraw + (int64_t)i * BQ + t), os, nz, ys, mean_out, std_out, cols, mean_cols, std_cols);
+                     ld_sc1(meanraw + (int64_t)i * BQ + t), os, nz, ys, mean_out, std_out, cols, mean_cols, std_cols,
+                     hmean, hstd, BQ);
     if (t == 0) atomicExch(&counters[(m.n_s * n_cb + i) * kGvCtrStride], 0u);
+    if constexpr (kSA) gp_sa_finish<BQ, SAM, SAK>(m, B, counters, *sa);
+}
+
+template <int D, int BQ>
+__global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
+                                                 int T, unsigned* counters, float* part, float* blk,
+                                                 float* meanraw, float* __restrict__ mean_out,
+                                                 float* __restrict__ std_out, GpCols cols,
+                                                 float* __restrict__ mean_cols, float* __restrict__ std_cols) {
+    gp_gemv_body<D, BQ>(m, B, xq, T, counters, part, blk, meanraw, mean_out, std_out, cols, mean_cols, std_cols,
+                        nullptr);
+}
+
+// RCBF_SAC.get_safe_action(obs) with the fitted GP in ONE launch (rcbf_gp_obs_safe_action): the GEMV of
+// the posterior on get_state(obs), then the last GP finisher solves the safe action (gp_sa_finish).
+template <int D, int BQ, int SAM, int SAK>
+__global__ void __launch_bounds__(256) k_gp_gemv_sa(rcbf_gp_model m, int64_t B, int T, unsigned* counters,
+                                                    float* part, float* blk, float* meanraw,
+                                                    float* __restrict__ mean_out, float* __restrict__ std_out,
+                                                    GpSafeAction sa) {
+    GpCols none{};
+    gp_gemv_body<D, BQ, SAM, SAK>(m, B, nullptr, T, counters, part, blk, meanraw, mean_out, std_out, none, nullptr,
+                                  nullptr, &sa);
 }
 
 // Split-K combine (the MFMA path, B > 8): one wave per (GP i, column block
@@ -719,9 +838,6 @@ __global__ void __launch_bounds__(256) k_gp_gemv(rcbf_gp_model m, int64_t B, con
 // fin (one column block per GP, a Lanczos factor): the wave also finishes its
 // query -- mean and std into the row and column outputs, the arithmetic of
 // gp_mean_std -- so no finish launch follows.
-__device__ __forceinline__ void gp_gv_finish(const rcbf_gp_model& m, int64_t B, int i, int b, float q, float mraw,
-                                             float os, float nz, float ys, float* mean_out, float* std_out,
-                                             const GpCols& cols, float* mean_cols, float* std_cols);
 
 __global__ void __launch_bounds__(256) k_gp_combine(rcbf_gp_model m, int64_t B, int n_cb, int n_split,
                                                     const float* __restrict__ qraw, float* __restrict__ partial,
@@ -849,8 +965,9 @@ int64_t rcbf_gp_workspace_floats(const rcbf_gp_model* m, int64_t B) {
     if (!m || B < 0 || m->C_pad < kGpCols || m->n_s < 1) return -1;
     const int64_t n_cb = m->C_pad / kGpCols;
     const int64_t cw = gp_counter_words(*m);
-    if (B <= kGvMaxB)  // GEMV: tile partials (32 columns x 8 queries), block sums, mean column
-        return cw + (int64_t)m->n_s * gp_gv_tiles(*m) * kGvMaxB * kGpCols + (int64_t)m->n_s * (n_cb + 1) * kGvMaxB;
+    if (B <= kGvMaxB)  // GEMV: tile partials (32 columns x 8 queries), block sums, mean column, the fused
+                       // safe action's mean / std hand-off
+        return cw + (int64_t)m->n_s * gp_gv_tiles(*m) * kGvMaxB * kGpCols + (int64_t)m->n_s * (n_cb + 3) * kGvMaxB;
     const int sk = gp_split(m, B);
     // partials for up to 2 launches per block, + means, + the split-K raw Q tiles
     return cw + (int64_t)m->n_s * (2 * n_cb + 1) * B + (sk > 1 ? (int64_t)sk * m->n_s * B * m->C_pad : 0);
@@ -990,6 +1107,78 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
                            n_part, partial, meanraw, gc, mean_cols, std_cols);
     }
     return launch_status();
+}
+
+
+int rcbf_gp_obs_safe_action(const rcbf_params* prm, const rcbf_gp_model* m, int64_t B, const float* obs,
+                            const float* u_rl, float* mean_out, float* std_out, float* u_out, float* u_host,
+                            uint32_t* done_word, uint32_t seq, int32_t* status_out, int32_t* fail_flag,
+                            float* workspace, hipStream_t stream) {
+    if (int e = check_prm(prm)) return e;
+    if (!m) return RCBF_E_NULL;
+    if (B != 1) return RCBF_E_BAD_SHAPE;  // the per-env-step query (main.py:93); batches take rcbf_gp_predict
+    if (m->n_s < 1 || m->n_s > 10 || m->N < 1 || m->N_pad % 32 || m->N_pad < m->N || m->r < 1 || m->r > m->N ||
+        m->C_pad % kGpCols || m->C_pad < m->r + 1)
+        return RCBF_E_BAD_SHAPE;
+    const bool cars = prm->mode == RCBF_MODE_SIMULATED_CARS;
+    if (m->n_s != (cars ? 10 : 3)) return RCBF_E_BAD_SHAPE;  // one GP per state dimension of the env
+    if (prm->solver != RCBF_SOLVER_ACTIVE_SET) return RCBF_E_BAD_MODE;
+    if (!obs || !u_rl || !workspace || !m->xt || !m->tn2 || !m->Rt || !m->x_std || !m->inv_sl || !m->outscale ||
+        !m->noise || !m->y_scale)
+        return RCBF_E_NULL;
+    if (!u_out && !u_host) return RCBF_E_NULL;  // nowhere to put the action
+    const int n_cb = m->C_pad / kGpCols;
+    const int T = gp_gv_tiles(*m);
+    unsigned* counters = reinterpret_cast<unsigned*>(workspace);
+    float* part = workspace + gp_counter_words(*m);
+    float* blk = part + (int64_t)m->n_s * T * kGvMaxB * kGpCols;
+    float* mraw = blk + (int64_t)m->n_s * n_cb * kGvMaxB;
+    GpSafeAction sa{};
+    sa.prm = *prm;
+    sa.obs = obs;
+    sa.u_rl = u_rl;
+    sa.hmean = mraw + (int64_t)m->n_s * kGvMaxB;
+    sa.hstd = sa.hmean + (int64_t)m->n_s * kGvMaxB;
+    sa.u_out = u_out;
+    sa.u_host = u_host;
+    sa.done_word = done_word;
+    sa.status_out = status_out;
+    sa.fail_flag = fail_flag;
+    sa.seq = seq;
+    dim3 gv((unsigned)T, (unsigned)m->n_s);
+#define RCBF_GVSA_L(DD, MODE_, K_)                                                                            \
+    hipLaunchKernelGGL((k_gp_gemv_sa<DD, 1, MODE_, K_>), gv, dim3(256), 0, stream, *m, B, T, counters, part, blk, \
+                       mraw, mean_out, std_out, sa)
+    if (cars) {
+        RCBF_GVSA_L(10, RCBF_MODE_SIMULATED_CARS, 1);
+    } else {
+        switch (prm->num_hazards) {
+            case 1: RCBF_GVSA_L(3, RCBF_MODE_UNICYCLE, 1); break;
+            case 2: RCBF_GVSA_L(3, RCBF_MODE_UNICYCLE, 2); break;
+            case 3: RCBF_GVSA_L(3, RCBF_MODE_UNICYCLE, 3); break;
+            case 4: RCBF_GVSA_L(3, RCBF_MODE_UNICYCLE, 4); break;
+            case 5: RCBF_GVSA_L(3, RCBF_MODE_UNICYCLE, 5); break;
+            case 6: RCBF_GVSA_L(3, RCBF_MODE_UNICYCLE, 6); break;
+            case 7: RCBF_GVSA_L(3, RCBF_MODE_UNICYCLE, 7); break;
+            case 8: RCBF_GVSA_L(3, RCBF_MODE_UNICYCLE, 8); break;
+            default: return RCBF_E_BAD_SHAPE;
+        }
+    }
+#undef RCBF_GVSA_L
+    if (int rc = launch_status()) return rc;
+    if (!done_word) return 0;
+    // the result is on the host once the word reads `seq` (the kernel's last stage publishes it system-wide);
+    // every 4096 polls ask the stream, so a failed kernel returns its error instead of spinning
+    volatile uint32_t* w = done_word;
+    for (uint32_t n = 1;; ++n) {
+        if (*w == seq) return 0;
+        __builtin_ia32_pause();
+        if ((n & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess) return *w == seq ? 0 : (int)hipErrorUnknown;
+            if (q != hipErrorNotReady) return (int)q;
+        }
+    }
 }
 
 }  // extern "C"

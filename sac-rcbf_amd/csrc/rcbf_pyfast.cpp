@@ -1,6 +1,6 @@
 // rcbf_pyfast.cpp -- CPython binding of the per-step entry points of
 // include/rcbf_hip.h for eager Python callers: rcbf_safe_step,
-// rcbf_safe_step_seq and rcbf_env_step_sync.
+// rcbf_safe_step_seq, rcbf_env_step_sync and rcbf_gp_obs_safe_action.
 //
 // BatchedEnv.safe_step is called once per env step; through ctypes its 21
 // arguments cost ~4 us of host time per call, comparable to the ~4.3 us
@@ -20,10 +20,12 @@ namespace {
 using SafeStepFn = decltype(&rcbf_safe_step);
 using SafeStepSeqFn = decltype(&rcbf_safe_step_seq);
 using EnvStepSyncFn = decltype(&rcbf_env_step_sync);
+using GpSafeActionFn = decltype(&rcbf_gp_obs_safe_action);
 
 SafeStepFn g_safe_step = nullptr;
 SafeStepSeqFn g_safe_step_seq = nullptr;
 EnvStepSyncFn g_env_step_sync = nullptr;
+GpSafeActionFn g_gp_safe_action = nullptr;
 
 bool as_u64(PyObject* o, unsigned long long* v) {
     if (o == Py_None) {
@@ -50,25 +52,47 @@ bool bound(const void* fn, const char* name) {
     return false;
 }
 
-// bind(addr_safe_step, addr_safe_step_seq, addr_env_step_sync) -> None
+// bind(addr_safe_step, addr_safe_step_seq, addr_env_step_sync, addr_gp_obs_safe_action) -> None
 PyObject* bind(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-    unsigned long long a[3];
-    if (!args_u64(args, nargs, 3, a, "bind")) return nullptr;
+    unsigned long long a[4];
+    if (!args_u64(args, nargs, 4, a, "bind")) return nullptr;
     g_safe_step = reinterpret_cast<SafeStepFn>(a[0]);
     g_safe_step_seq = reinterpret_cast<SafeStepSeqFn>(a[1]);
     g_env_step_sync = reinterpret_cast<EnvStepSyncFn>(a[2]);
+    g_gp_safe_action = reinterpret_cast<GpSafeActionFn>(a[3]);
     Py_RETURN_NONE;
 }
 
-// bound() -> (addr_safe_step, addr_safe_step_seq, addr_env_step_sync): what bind() stored
+// bound() -> the entry-point addresses bind() stored, in bind()'s order
 PyObject* bound_addrs(PyObject*, PyObject* const*, Py_ssize_t nargs) {
     if (nargs != 0) {
         PyErr_SetString(PyExc_TypeError, "bound() takes no arguments");
         return nullptr;
     }
-    return Py_BuildValue("(KKK)", (unsigned long long)(uintptr_t)g_safe_step,
+    return Py_BuildValue("(KKKK)", (unsigned long long)(uintptr_t)g_safe_step,
                          (unsigned long long)(uintptr_t)g_safe_step_seq,
-                         (unsigned long long)(uintptr_t)g_env_step_sync);
+                         (unsigned long long)(uintptr_t)g_env_step_sync,
+                         (unsigned long long)(uintptr_t)g_gp_safe_action);
+}
+
+// gp_obs_safe_action(prm, model, obs, u_rl, workspace, stream, host_block, seq) -> int: rcbf_gp_obs_safe_action
+// at B = 1 with the action, the QP status and the completion word in one pinned host block (bytes 0, 32, 64);
+// returns once the word reads seq (the action is then on the host)
+PyObject* gp_obs_safe_action(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+    unsigned long long a[8];
+    if (!args_u64(args, nargs, 8, a, "gp_obs_safe_action") ||
+        !bound((const void*)g_gp_safe_action, "gp_obs_safe_action"))
+        return nullptr;
+    int rc;
+    char* host = reinterpret_cast<char*>(a[6]);
+    Py_BEGIN_ALLOW_THREADS
+    rc = g_gp_safe_action(reinterpret_cast<const rcbf_params*>(a[0]), reinterpret_cast<const rcbf_gp_model*>(a[1]), 1,
+                          reinterpret_cast<const float*>(a[2]), reinterpret_cast<const float*>(a[3]), nullptr,
+                          nullptr, nullptr, reinterpret_cast<float*>(host), reinterpret_cast<uint32_t*>(host + 64),
+                          (uint32_t)a[7], reinterpret_cast<int32_t*>(host + 32), nullptr,
+                          reinterpret_cast<float*>(a[4]), reinterpret_cast<hipStream_t>(a[5]));
+    Py_END_ALLOW_THREADS
+    return PyLong_FromLong(rc);
 }
 
 // safe_step(prm, B, x, aux, step, episode, u_rl, mu, sigma, obs, u_out, reward,
@@ -163,6 +187,8 @@ PyMethodDef kMethods[] = {
      "rcbf_safe_step_seq with integer pointer arguments and a sequence of u_rl pointers"},
     {"env_step_sync", RCBF_FASTCALL(env_step_sync), METH_FASTCALL,
      "rcbf_env_step_sync (launch + stream synchronise) with integer pointer arguments"},
+    {"gp_obs_safe_action", RCBF_FASTCALL(gp_obs_safe_action), METH_FASTCALL,
+     "rcbf_gp_obs_safe_action at B = 1 into a pinned host block, with integer pointer arguments"},
     {nullptr, nullptr, 0, nullptr}};
 #undef RCBF_FASTCALL
 

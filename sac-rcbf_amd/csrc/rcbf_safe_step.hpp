@@ -160,8 +160,10 @@ __device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_
 // BS: workgroup size (block_for_envs).  SPAN = true (rcbf_safe_step_span, a
 // measurement entry point of the product library): lane 0 of every wave
 // writes the chip clock (s_memrealtime, 100 MHz) at its start and after its
-// own stores have completed to stamp_buf[2 w], [2 w + 1]; every other
-// instruction is the product's.
+// own stores have completed to stamp_buf[4 w], [4 w + 1], and the shader
+// clock (s_memtime) at the same two points to stamp_buf[4 w + 2], [4 w + 3]
+// (the clock the wave ran at is delta(s_memtime) / delta(s_memrealtime) x
+// 100 MHz); every other instruction is the product's.
 // Argument order: B and the pointers of the first loads lead (one 64-B line
 // of the argument block, which the launch can preload into SGPRs), the
 // parameter block comes last.
@@ -179,8 +181,11 @@ __global__ void __launch_bounds__(BS) k_safe_step(int64_t B, double* __restrict_
     using D = Dims<MODE, K>;
     int64_t i = env_index<BS>();
     if (i >= B) return;
-    unsigned long long span_t0 = 0;
-    if constexpr (SPAN) span_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long span_t0 = 0, span_c0 = 0;
+    if constexpr (SPAN) {
+        span_t0 = __builtin_amdgcn_s_memrealtime();
+        span_c0 = __builtin_amdgcn_s_memtime();
+    }
     Stamps<ST> stamps;
     stamps.buf = stamp_buf;
     stamps.mark(0, false);
@@ -301,10 +306,12 @@ __global__ void __launch_bounds__(BS) k_safe_step(int64_t B, double* __restrict_
     if constexpr (SPAN) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have landed
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime();
         if ((threadIdx.x & 63) == 0) {
             const int64_t w = ((int64_t)blockIdx.x * BS + threadIdx.x) >> 6;
             typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
-            *reinterpret_cast<u2*>(stamp_buf + 2 * w) = u2{span_t0, t1};
+            *reinterpret_cast<u2*>(stamp_buf + 4 * w) = u2{span_t0, t1};
+            *reinterpret_cast<u2*>(stamp_buf + 4 * w + 2) = u2{span_c0, c1};
         }
     }
 }

@@ -94,6 +94,7 @@ SIGNATURES = {
     "rcbf_ring_scatter_f64": [_P, _I64, _I64, _I64, _P, _I64, _P],
     "rcbf_gather_rows_f64": [_P, _P, _I64, _P, _I64, _P],
     "rcbf_gp_predict": [_GPM, _I64, _P, _P, _P, _P, _P],
+    "rcbf_gp_obs_safe_action": [_PRM, _GPM, _I64, _P, _P, _P, _P, _P, _P, _P, ctypes.c_uint32, _P, _P, _P, _P],
     "rcbf_gp_predict_cols": [_GPM, _I64, _P, _P, _P, _P, _I32, _P, _P, _P, _P],
     "rcbf_obs_safe_action_backward": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_safe_action_jac": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
@@ -160,7 +161,7 @@ def load():
     return lib
 
 
-FAST_ENTRY_POINTS = ("rcbf_safe_step", "rcbf_safe_step_seq", "rcbf_env_step_sync")
+FAST_ENTRY_POINTS = ("rcbf_safe_step", "rcbf_safe_step_seq", "rcbf_env_step_sync", "rcbf_gp_obs_safe_action")
 _fast = None
 
 

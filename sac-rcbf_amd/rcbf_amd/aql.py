@@ -22,6 +22,7 @@ import torch
 from . import _lib
 
 PROFILE = 1  # RCBF_AQL_PROFILE
+PROFILE_ENDS = 64  # RCBF_AQL_PROFILE_ENDS: timestamps of the first and last dispatch only
 
 
 def _bind():
@@ -85,9 +86,9 @@ class AqlQueue:
         if span is not None:
             nw = (env.num_envs + 63) // 64
             if not (torch.is_tensor(span) and span.dtype == torch.int64 and span.device == env.device
-                    and span.is_contiguous() and span.numel() >= 2 * nw * K):
-                raise ValueError(f"span must be a contiguous int64 tensor of >= {2 * nw * K} entries "
-                                 f"(K blocks of ceil(B / 64) x 2) on {env.device}")
+                    and span.is_contiguous() and span.numel() >= 4 * nw * K):
+                raise ValueError(f"span must be a contiguous int64 tensor of >= {4 * nw * K} entries "
+                                 f"(K blocks of ceil(B / 64) x 4) on {env.device}")
         a = env._step_args(layer, o, auto_reset)
         arr = (ctypes.c_void_p * len(us))(*[u.data_ptr() for u in us])
         h = ctypes.c_void_p()

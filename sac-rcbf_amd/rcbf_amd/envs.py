@@ -336,8 +336,9 @@ class BatchedEnv:
     def safe_step_span(self, u_rl, layer, span, mean=None, sigma=None, auto_reset=True, outputs=None,
                        prior_layout="rows"):
         """safe_step through the measurement entry point rcbf_safe_step_span:
-        the same step, plus each wave's start / end chip-clock stamps in
-        `span` ((ceil(B / 64), 2) int64 on this device).  bench.py only."""
+        the same step, plus each wave's start / end chip-clock stamps and
+        shader-clock stamps in `span` ((ceil(B / 64), 4) int64 on this
+        device: realtime start, end, memtime start, end).  bench.py only."""
         o = outputs if outputs is not None else self.make_outputs()
         u = self._u_arg(u_rl)
         cols = prior_layout == "cols"
@@ -347,8 +348,8 @@ class BatchedEnv:
             mean, sigma = self._prior_arg(mean, "mean"), self._prior_arg(sigma, "sigma")
         nw = (self.num_envs + 63) // 64
         if not (torch.is_tensor(span) and span.dtype == torch.int64 and span.device == self.device
-                and span.is_contiguous() and span.numel() >= 2 * nw):
-            raise ValueError(f"span must be a contiguous int64 tensor of >= {2 * nw} entries on {self.device}")
+                and span.is_contiguous() and span.numel() >= 4 * nw):
+            raise ValueError(f"span must be a contiguous int64 tensor of >= {4 * nw} entries on {self.device}")
         a = self._step_args(layer, o, auto_reset)
         rc = _lib.load().rcbf_safe_step_span(
             ctypes.byref(layer._prm), self.num_envs, *[v or None for v in a[2:6]], u.data_ptr(),

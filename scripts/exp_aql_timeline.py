@@ -103,7 +103,7 @@ def main():
     res["idle_synchronize_us"] = round((time.perf_counter() - t0) * 1e4, 3)
     # span-stamped AQL run of 20 steps: per step first start / last end (100 MHz chip clock)
     nw = B // 64
-    span = torch.zeros(20, nw, 2, dtype=torch.int64, device=dev)
+    span = torch.zeros(20, nw, 4, dtype=torch.int64, device=dev)
     sp = q.safe_step_plan(env, pool, layer, steps=20, outputs=outs, span=span)
     for rep in range(3):
         torch.cuda.synchronize()
@@ -139,7 +139,7 @@ def main():
                                          "gap_us": [round(v, 2) for v in (st[1:] - en[:-1]) * .01]}
     # fence-scope variants of the AQL plan (flags of rcbf_aql_safe_step_plan): wall of K = 1 / 20 and the
     # span-stamped 20-step run (first span, median gap)
-    for fl in (0, 2, 4, 6, 14):
+    for fl in (0, 2, 16, 32, 8):
         p1 = q.safe_step_plan(env, pool, layer, steps=1, outputs=outs, fence_flags=fl)
         p20 = q.safe_step_plan(env, pool, layer, steps=20, outputs=outs, fence_flags=fl)
         s20 = q.safe_step_plan(env, pool, layer, steps=20, outputs=outs, span=span, fence_flags=fl)

@@ -63,15 +63,22 @@ for step in "$@"; do
     pytest) run pytest 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;
     driver) run driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    drvgraph) run drvgraph 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --launch graph ;;
+    recdrv)  # the driver's command with its roofline record (per-step GPU time, dispatch timestamps, span stamps, clock)
+      run recdrv 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline \
+        --record "$OUT/roofline_record_driver_form_aql_cars_B65536_$TAG.json" ;;
+    recdef) run recdef 300 python bench.py --no-cpu-baseline --record "$OUT/roofline_record_aql_cars_B65536_$TAG.json" ;;
+    pmcbusy)  # GRBM_GUI_ACTIVE / SQ_BUSY_CYCLES pass of the driver's command -> busy us per dispatch (needs recdrv first)
+      run pmcbusy 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d "$OUT/pmcbusy" -o run -- \
+        python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-span
+      [ -f "$OUT/pmcbusy/run_counter_collection.csv" ] && python scripts/pmc_busy.py "$OUT/pmcbusy/run_counter_collection.csv" \
+        "$(wl_kernel cars)" "$OUT/roofline_record_driver_form_aql_cars_B65536_$TAG.json" \
+        "$OUT/pmc_busy_driver_form_aql_cars_B65536_$TAG.json" > /dev/null ;;
     benchx) run benchx 600 python bench.py --extra --no-cpu-baseline ;;
     aqltest) run aqltest 300 python -u -m pytest tests/test_gpu_aql.py -q -rf --timeout 200 --timeout-method thread ;;
     aqltl) run aqltl 300 python -u scripts/exp_aql_timeline.py ;;
     drvaql) run drvaql 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --launch aql ;;
     benchaql) run benchaql 300 python bench.py --no-cpu-baseline --launch aql ;;
-    profdrvaql)  # the driver's command with the AQL launch, traced (rocprofv3 intercepts the library's HSA queue too)
-      run profdrvaql 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profdrvaql" -o run -- \
-        python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --launch aql
-      [ -f "$OUT/profdrvaql/run_kernel_stats.csv" ] && cp "$OUT/profdrvaql/run_kernel_stats.csv" "$OUT/kernel_stats_driver_form_aql_cars_B65536_$TAG.csv" ;;
     sweep)  # waves per SIMD: B = 32768 (half the SIMDs), 65536 (one wave each), 98304, 131072 (two)
       for w in cars uni3 uni5; do for b in 32768 65536 98304 131072; do
         run "sweep_${w}_$b" 300 python bench.py --no-cpu-baseline --batch "$b" $(wl_args "$w")
@@ -84,12 +91,12 @@ for step in "$@"; do
       [ -f "$OUT/prof_$wl/run_kernel_trace.csv" ] && python scripts/trace_summary.py "$OUT/prof_$wl/run_kernel_trace.csv" \
         "$(wl_kernel "$wl")" "$OUT/$(wl_name "$wl")_kernel_trace_summary.json"
       [ -f "$OUT/prof_$wl/run_kernel_stats.csv" ] && cp "$OUT/prof_$wl/run_kernel_stats.csv" "$OUT/kernel_stats_$(wl_name "$wl")_$TAG.csv" ;;
-    profdrv)  # the driver's own command under the tracer
+    profdrv)  # the driver's own command under the tracer (the AQL launch: rocprofv3 intercepts the library's queue)
       run profdrv 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profdrv" -o run -- \
         python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
       [ -f "$OUT/profdrv/run_kernel_trace.csv" ] && python scripts/trace_summary.py "$OUT/profdrv/run_kernel_trace.csv" \
-        "$(wl_kernel cars)" "$OUT/cars_B65536_driver_form_kernel_trace_summary.json"
-      [ -f "$OUT/profdrv/run_kernel_stats.csv" ] && cp "$OUT/profdrv/run_kernel_stats.csv" "$OUT/kernel_stats_driver_form_cars_B65536_$TAG.csv" ;;
+        "$(wl_kernel cars)" "$OUT/cars_B65536_driver_form_aql_kernel_trace_summary.json"
+      [ -f "$OUT/profdrv/run_kernel_stats.csv" ] && cp "$OUT/profdrv/run_kernel_stats.csv" "$OUT/kernel_stats_driver_form_aql_cars_B65536_$TAG.csv" ;;
     pmc_*)
       run "pmcf_$wl" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcf_$wl" -o run -- \
         python3 bench.py --no-cpu-baseline --no-graph --steps 50 --warmup 5 $(wl_args "$wl")

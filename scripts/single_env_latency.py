@@ -4,7 +4,9 @@ numpy action, CBFQPLayer.get_safe_action on 1-D device tensors, and
 RCBF_SAC.get_safe_action (rcbf_amd.sac_cbf) on one observation, without and
 with a fitted GP (300 points, Lanczos rank 16, the training-loop test's
 setting): back to back, and as select_action takes it (each call followed by
-.cpu(), i.e. one host round trip), with its three launches timed apart.
+.cpu(), i.e. one host round trip), with its three launches timed apart;
+and at the reference's N = 3000 (LOVE rank 100) the one-launch host-result
+path (sac_cbf.get_safe_action_host) against the three launches + .cpu().
 Prints one JSON line of microseconds per call (median of 5 runs of 200 calls)."""
 import json
 import os
@@ -88,6 +90,23 @@ def main():
         out[f"{name}_gp_get_state_us"] = per_call_us(lambda: gdm.get_state(o2))
         out[f"{name}_gp_predict_us"] = per_call_us(lambda: gpm.predict(s2))
         out[f"{name}_to_host_us"] = per_call_us(lambda: u.cpu())
+        # the reference's gp_model_size N = 3000 with LOVE rank 100, select_action's call
+        # as ONE launch whose action lands in pinned host memory (get_safe_action_host) vs the three launches
+        # + .cpu()
+        from rcbf_amd import gp
+        from rcbf_amd.sac_cbf import get_safe_action_host
+        n_s = gdm.n_s
+        xb = rng.uniform(-1, 1, (3000, n_s)) * (30.0 if n_s == 10 else 3.0)
+        gdm.disturb_estimators = gp.GPDisturbanceModel(xb, 0.05 * np.sin(xb) + rng.normal(0, 0.02, xb.shape),
+                                                       [(1.3, 0.2, 0.05)] * n_s, rank=gp.love_rank(3000))
+        assert gdm.disturb_estimators.r <= 100 and gdm.disturb_estimators.rank == 100
+        a = get_safe_action_host(layer, ot, u, gdm)
+        b = get_safe_action(layer, ot, u, gdm).cpu().numpy()
+        assert np.array_equal(a, b)
+        out[f"{name}_gp3000_three_launches_to_host_us"] = per_call_us(
+            lambda: get_safe_action(layer, ot, u, gdm).cpu())
+        out[f"{name}_gp3000_one_launch_host_result_us"] = per_call_us(
+            lambda: get_safe_action_host(layer, ot, u, gdm))
     print(json.dumps(out), flush=True)
 
 

@@ -104,15 +104,17 @@ def test_profiled_plan_times_and_span(queue):
     _assert_same(_snapshot(e1, o1), _snapshot(e2, o2))
     # the span instantiation through the queue: the same step plus per-wave chip-clock stamps
     nw = B // 64
-    span = torch.zeros(nw, 2, dtype=torch.int64, device="cuda")
+    span = torch.zeros(nw, 4, dtype=torch.int64, device="cuda")
     sp = queue.safe_step_plan(e2, pool[:1], l2, steps=1, outputs=o2, span=span)
     sp.run()
     e1.safe_step(pool[0], l1, outputs=o1)
     torch.cuda.synchronize()
     _assert_same(_snapshot(e1, o1), _snapshot(e2, o2))
     s = span.cpu().numpy()
-    assert (s[:, 0] > 0).all() and (s[:, 1] >= s[:, 0]).all()
+    assert (s[:, 0] > 0).all() and (s[:, 1] >= s[:, 0]).all() and (s[:, 3] > s[:, 2]).all()
     assert (s[:, 1].max() - s[:, 0].min()) < 100_000  # < 1 ms of 100 MHz ticks
+    clk = (s[:, 3] - s[:, 2]) / np.maximum(s[:, 1] - s[:, 0], 1) * 100.0  # MHz
+    assert 500 < np.median(clk) < 3000
     e2.check_failures()
 
 
@@ -124,4 +126,4 @@ def test_plan_argument_errors(queue):
     with pytest.raises(ValueError):
         queue.safe_step_plan(e1, [], l1, steps=3)
     with pytest.raises(ValueError):  # a span plan needs K blocks of stamps
-        queue.safe_step_plan(e1, pool, l1, steps=2, span=torch.zeros(4, 2, dtype=torch.int64, device="cuda"))
+        queue.safe_step_plan(e1, pool, l1, steps=2, span=torch.zeros(4, 4, dtype=torch.int64, device="cuda"))

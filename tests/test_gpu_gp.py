@@ -326,7 +326,7 @@ def test_gp_gemv_handoff_across_calls(rank):
             _check(outs[j][0].cpu().numpy(), outs[j][1].cpu().numpy(), mo[offs[j]:offs[j + 1]], so[offs[j]:offs[j + 1]])
     # the arrival counters (one per 128-B line: n_s (n_cb + 1) of them) and the fail word's line lead the
     # workspace and are zero again
-    n_ctr = model.n_s * (model._m.C_pad // 128 + 1) * 32 + 32
+    n_ctr = model.n_s * (model._m.C_pad // 128 + 1) * 32 + 64
     assert int(ws.view(torch.int32)[:n_ctr].abs().sum()) == 0
     model.check_failures()
 
@@ -422,3 +422,70 @@ def test_sac_safe_action_with_gp_is_the_reference_three_calls(mode, k):
         (out2 * w).sum().backward()
         assert torch.equal(out1.detach(), out2.detach()) and torch.equal(u1.grad, u2.grad), B
         assert bool((out1.detach() != ua).any()) or B == 1  # the filter is active on part of the batch
+
+
+@pytest.mark.parametrize("mode,k,rank", [("SimulatedCars", 1, "love"), ("Unicycle", 3, "love"), ("Unicycle", 5, "love"),
+                                         ("SimulatedCars", 1, "exact"), ("Unicycle", 5, "exact")])
+def test_one_launch_safe_action_with_gp_equals_three_launches(mode, k, rank):
+    """rcbf_gp_obs_safe_action -- get_state(obs), the GP
+    posterior GEMV and the safe action in ONE launch, the action written to
+    pinned host memory behind a completion word (sac_cbf.get_safe_action_host)
+    -- equals the three-launch path (rcbf_state_from_obs -> rcbf_gp_predict ->
+    rcbf_obs_safe_action, itself bit-equal to the reference's three calls)
+    bit for bit, over 64 single observations with states spread so the filter
+    is active on part of them, for a Lanczos (one column block) and an exact
+    (multi-block: the second hand-off level) factor; the posterior rows and
+    the counters are checked too."""
+    from rcbf_amd import gp
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.envs import BatchedSimulatedCarsEnv, BatchedUnicycleEnv
+    from rcbf_amd.sac_cbf import get_safe_action, get_safe_action_host
+    rng = np.random.default_rng(31 + k)
+    N = 1100
+    if mode == "SimulatedCars":
+        env = BatchedSimulatedCarsEnv(4)
+        x = np.tile(np.array([34.0, 30, 28, 30, 22, 30, 16, 35, 10, 30]), (N, 1)) + rng.normal(0, 1.5, (N, 10))
+    else:
+        env = BatchedUnicycleEnv(4, hazards_locations=O.UNI["hazards"][:k])
+        x = np.stack([rng.uniform(-3, 3, N), rng.uniform(-3, 3, N), rng.uniform(-np.pi, np.pi, N)], 1)
+    n_s = x.shape[1]
+    dm = DynamicsModel(env, types.SimpleNamespace(cuda=True, gp_model_size=N))
+    hyper = [(1.3, 0.2, 0.05)] * n_s
+    dm.disturb_estimators = gp.GPDisturbanceModel(x, 0.05 * np.sin(x) + rng.normal(0, 0.02, x.shape), hyper,
+                                                  rank=gp.love_rank(N) if rank == "love" else None)
+    gpm = dm.disturb_estimators
+    layer = CBFQPLayer(env, types.SimpleNamespace(cuda=True), gamma_b=20.0)
+    active = 0
+    for j in range(64):
+        idx = rng.integers(0, N)
+        obs = (O.cars_obs(x[idx:idx + 1]) if mode == "SimulatedCars" else O.uni_obs(x[idx:idx + 1])).astype(np.float32)
+        ob = torch.as_tensor(obs[0], device="cuda")
+        ua = torch.as_tensor(rng.uniform(-1, 1, env.n_u).astype(np.float32), device="cuda")
+        ref = get_safe_action(layer, ob, ua, dm).cpu().numpy()
+        got = get_safe_action_host(layer, ob, ua, dm)
+        assert got.shape == ref.shape and np.array_equal(got, ref), (j, got, ref)
+        active += int(not np.array_equal(ref, ua.cpu().numpy()))
+    assert active > 0
+    # the posterior rows the fused kernel hands to its last stage equal rcbf_gp_predict's
+    import ctypes
+    from rcbf_amd import _lib
+    ob = torch.as_tensor(obs, device="cuda")
+    ua = torch.as_tensor(rng.uniform(-1, 1, (1, env.n_u)).astype(np.float32), device="cuda")
+    mo, so, uo = torch.empty(1, n_s, device="cuda"), torch.empty(1, n_s, device="cuda"), torch.empty(1, env.n_u, device="cuda")
+    ws, stream = gpm._workspace(1)
+    rc = _lib.load().rcbf_gp_obs_safe_action(ctypes.byref(layer._prm), ctypes.byref(gpm._m), 1, _lib.ptr(ob), _lib.ptr(ua),
+                                             _lib.ptr(mo), _lib.ptr(so), _lib.ptr(uo), None, None, 0, None, None,
+                                             _lib.ptr(ws), stream)
+    assert rc == 0
+    m2, s2 = gpm.predict(dm.get_state(ob))
+    torch.cuda.synchronize()
+    assert torch.equal(mo, m2) and torch.equal(so, s2)
+    assert torch.equal(uo, get_safe_action(layer, ob, ua, dm))
+    gpm.check_failures()
+    n_ctr = gpm.n_s * (gpm._m.C_pad // 128 + 1) * 32 + 64
+    assert int(ws.view(torch.int32)[:n_ctr].abs().sum()) == 0
+    # B != 1 and another solver are refused (the wrapper then takes the three launches)
+    assert _lib.load().rcbf_gp_obs_safe_action(ctypes.byref(layer._prm), ctypes.byref(gpm._m), 2, _lib.ptr(ob),
+                                               _lib.ptr(ua), None, None, _lib.ptr(uo), None, None, 0, None, None,
+                                               _lib.ptr(ws), stream) == 1002

@@ -288,7 +288,7 @@ def test_span_entry_point_is_the_product_step(mode, k, B):
     b.load_state(a.state, a.aux, a.step_count)
     b.episode.copy_(a.episode)
     nw = (B + 63) // 64
-    span = torch.zeros(nw, 2, dtype=torch.int64, device=a.device)
+    span = torch.zeros(nw, 4, dtype=torch.int64, device=a.device)
     oa, ob = a.make_outputs(), b.make_outputs()
     for j in range(6):
         u = (torch.rand(B, a.n_u, device=a.device, generator=gen) * 2 - 1).contiguous()

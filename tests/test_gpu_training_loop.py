@@ -116,8 +116,9 @@ class _Agent:
             action = m if evaluate else a
         torch.cuda.synchronize()  # the policy's launches are not the safety layer's time
         t0 = time.perf_counter()
-        safe = self.get_safe_action(state, action, dynamics_model)
-        out = safe.detach().cpu().numpy()
+        # the per-env-step path: with the fitted GP one launch that leaves the action in pinned host memory
+        from rcbf_amd.sac_cbf import get_safe_action_host
+        out = get_safe_action_host(self.cbf_layer, state, action, dynamics_model)
         self.safe_action_s.append(time.perf_counter() - t0)
         return out[0] if expand else out
 
