@@ -89,7 +89,7 @@ def parse():
                     help="a BASELINE.json config (0: the headline, cars B = 65536 per GPU): 1 cars, one env; "
                          "2 cars B = 4096; 3 unicycle (3 hazards) B = 4096; 4 cars B = 262144 split over the GPUs "
                          "(strong); 5 cars B = 4096 SAC-update safe action, forward + backward")
-    ap.add_argument("--workload", default="step", choices=["step", "sac_update"],
+    ap.add_argument("--workload", default="step", choices=["step", "sac_update", "closed_loop"],
                     help="step: the fused safe step; sac_update: RCBF_SAC.get_safe_action on a replay batch "
                          "forward + backward (rcbf_obs_safe_action + its backward, config 5)")
     ap.add_argument("--no-span", action="store_true", help="skip the untimed in-kernel span measurement")
@@ -105,7 +105,7 @@ def parse():
                          "the backward applies it (rcbf_safe_action_apply_jac), as the autograd op runs it; resolve "
                          "= the plain forward and the re-solving backward (rcbf_obs_safe_action_backward)")
     args = ap.parse_args()
-    preset = {1: dict(env="SimulatedCars", batch=1, workload="step"),
+    preset = {1: dict(env="SimulatedCars", batch=1, workload="closed_loop"),
               2: dict(env="SimulatedCars", batch=4096, workload="step", prior="rows", prior_values="maxstd"),
               3: dict(env="Unicycle", hazards=3, batch=4096, workload="step"),
               4: dict(env="SimulatedCars", batch=262144, scaling="strong", workload="step"),
@@ -424,8 +424,8 @@ def pin_host_cores(local, n):
 
 METRICS = {
     0: "safe env steps/sec (dynamics+CBF-QP) at batch 65536, 1/2/4/8 MI355X",
-    1: "safe env steps/sec (dynamics+CBF-QP), config 1: SimulatedCars, 1 env (the fused CBFQPLayer step; config 1's "
-       "Cascade closed loop is tests/test_gpu_parity.py::test_closed_loop_config1)",
+    1: "safe env steps/sec (dynamics+CBF-QP), config 1: SimulatedCars, 1 env, 300-step episode, the Cascade "
+       "closed loop with the hand controller",
     2: "safe env steps/sec (dynamics+CBF-QP), config 2: SimulatedCars batch 4096, 1 MI355X",
     3: "safe env steps/sec (dynamics+CBF-QP), config 3: Unicycle (3 hazards) batch 4096, 1 MI355X",
     4: "safe env steps/sec (dynamics+CBF-QP), config 4: SimulatedCars batch 262144 over the GPUs",
@@ -638,6 +638,8 @@ def main():
                                                             args.batch)}
         print(json.dumps(out), flush=True)
         return
+    if args.workload == "closed_loop":
+        return bench_closed_loop(args)
     from rcbf_amd import shard
     rank, local, world = shard.world_info()
     if world == 1 and args.gpus > 1:
@@ -857,6 +859,100 @@ def write_record(args, rec, short, B, bps, kern_ms, aql_times, span, stamps):
     os.makedirs(os.path.dirname(os.path.abspath(args.record)), exist_ok=True)
     with open(args.record, "w") as f:
         json.dump(out, f, indent=1)
+
+
+def bench_closed_loop(args):
+    """BASELINE config 1 as the reference runs it (envs/simulated_cars_env.py:161-228): ONE SimulatedCars env,
+    the hand controller (:195-199), DynamicsModel.get_state / predict_disturbance (the prior) and
+    CascadeCBFLayer(env, gamma_b=20, k_d=3).get_u_safe (cbf_qp.py:29-53) on rcbf_cascade_u_safe_sync, then
+    env.step(u_nom + u_safe) on rcbf_env_step_sync -- every call the reference's own surface, per step.
+    Timed: exactly --steps closed-loop steps (episodes of 300 from the golden reset, resetting when done),
+    after --warmup untimed ones.  Then, untimed, one full episode is checked against the reference's own
+    closed loop (tests/golden/closed_loop_cars.npz) and the C oracle's loop is timed on one core beside it.
+    One process (the loop is single-env, host-driven: replicas only across GPUs)."""
+    import types
+    from rcbf_amd.cbf_qp import CascadeCBFLayer
+    from rcbf_amd.dynamics import DynamicsModel
+    from rcbf_amd.envs import SimulatedCarsEnv
+    gold = np.load(os.path.join(ROOT, "tests", "golden", "closed_loop_cars.npz"))
+    noise = float(gold["noise"])
+    env = SimulatedCarsEnv()
+    dm = DynamicsModel(env, types.SimpleNamespace(gp_model_size=2000, cuda=False))
+    layer = CascadeCBFLayer(env, gamma_b=20.0, k_d=3.0)
+
+    def reset():
+        env._b.reset(noise=np.array([noise]))  # the golden episode's velocity draw (:120)
+        return env._get_obs()
+
+    def controller(s):  # simulated_cars_env.py:195-199
+        a = np.array([1.0 * (s[4] - s[6] - 0.4) * (s[4] - s[6] - 0.4 < 0)])
+        a += np.array([1.0 * (s[8] - s[6] + 0.4) * (s[8] - s[6] + 0.4 > 0)])
+        return a
+
+    def run(n, obs, record=None):
+        for _ in range(n):
+            state = dm.get_state(obs)
+            u = controller(state)
+            mean, std = dm.predict_disturbance(state)
+            us = layer.get_u_safe(u, state, mean, std)
+            obs, r, done, info = env.step(u + us)
+            if record is not None:
+                record.append((u[0], us[0], env.state.copy()))
+            if done:
+                obs = reset()
+        return obs
+
+    obs = run(max(args.warmup, 1), reset())
+    obs = reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    obs = run(args.steps, obs)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # parity, untimed: one whole episode against the reference's own loop
+    rec = []
+    run(300, reset(), rec)
+    u_nom = np.array([r[0] for r in rec]); u_safe = np.array([r[1] for r in rec])
+    xs = np.array([r[2] for r in rec])
+
+    def rel(a, b):
+        return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b))))
+    parity = {"u_nom": rel(u_nom, gold["u_nom"][:, 0]), "u_safe": rel(u_safe, gold["u_safe"][:, 0]),
+              "state": rel(xs, gold["state"][1:]), "steps": 300,
+              "against": "tests/golden/closed_loop_cars.npz (the reference's own closed loop, exact QP)"}
+    ok = parity["u_safe"] <= 1e-6 and parity["state"] <= 1e-8
+    line = {"metric": METRICS.get(1, METRICS[0]), "value": round(args.steps / el, 1), "unit": "safe env steps/s",
+            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64 rows / f64 QP / f64 env",
+            "data": "the reference's config-1 episode: golden reset draw, the hand controller's actions",
+            "config": {"workload": "SimulatedCars Cascade closed loop (config 1, envs/simulated_cars_env.py:161-228): "
+                                   "1 env, hand controller + DynamicsModel prior + CascadeCBFLayer.get_u_safe "
+                                   "(rcbf_cascade_u_safe_sync) + env.step (rcbf_env_step_sync), host-driven per step",
+                       "baseline_config": 1, "batch_per_gpu": 1, "global_batch": 1, "env": "SimulatedCars",
+                       "parallelism": "single env (replicas only)"},
+            "parity": dict(parity, ok=ok)}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_closed_loop(noise, args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+    if not ok:
+        raise SystemExit(f"config-1 closed loop differs from the reference's: {parity}")
+
+
+def cpu_closed_loop(noise, seconds):
+    """The C oracle's config-1 closed loop (oracle_cars_cascade_loop: the same controller, Cascade QP and env
+    in fp64 C) on ONE core, repeated for ~seconds / 5."""
+    from oracle import c_oracle as C
+    budget = max(1.0, seconds / 5)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        C.cars_cascade_loop(noise, 300)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget:
+            break
+    return {"value": round(n * 300 / el, 1), "unit": "safe env steps/s", "cores": 1, "kind": "port",
+            "sample": f"C oracle closed loop (oracle/rcbf_oracle.c oracle_cars_cascade_loop), {n} episodes of 300 "
+                      f"steps in {el:.2f} s on one thread"}
 
 
 def unicycle_hazards(k):

@@ -215,6 +215,18 @@ int rcbf_cascade_u_safe(const rcbf_params* prm, int64_t B, const double* u_nom,
                         double* u_safe_out, int32_t* status_out, int32_t* fail_flag,
                         double* eps_out, hipStream_t stream);
 
+/* rcbf_cascade_u_safe for B <= 256 samples in ONE workgroup that ends by
+ * storing `seq` into done_word (pinned host memory, system scope); the call
+ * returns when it reads `seq`.  Every array may be pinned host memory
+ * (rcbf_host_alloc: the kernel reads and writes it in place) or device
+ * memory, so the reference's single-sample get_u_safe of its per-step loop
+ * (envs/simulated_cars_env.py:213, cbf_qp.py:29-53) costs no copy and no
+ * stream synchronisation.  status_out, eps_out, mu, sigma [nullable]. */
+int rcbf_cascade_u_safe_sync(const rcbf_params* prm, int64_t B, const double* u_nom,
+                             const double* x, const double* mu, const double* sigma,
+                             double* u_safe_out, int32_t* status_out, double* eps_out,
+                             uint32_t* done_word, uint32_t seq, hipStream_t stream);
+
 /* ---------------------------------------------------------------------- */
 /* GP disturbance posterior                              */
 /* ---------------------------------------------------------------------- */

@@ -25,6 +25,7 @@ def lib():
                                             P, P, P, P, P, ctypes.c_int]
         _lib.oracle_safe_step.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double, ctypes.c_int64,
                                           P, P, P, P, P, P, P, P, ctypes.c_int]
+        _lib.oracle_cars_cascade_loop.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_double, P, P, P]
         _lib.oracle_safe_step_ex.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double, ctypes.c_int64,
                                              P, P, P, P, P, P, P, P, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int]
         _lib.oracle_safe_action_grad.argtypes = [ctypes.c_int, ctypes.c_int, P, ctypes.c_double, ctypes.c_int64,
@@ -115,3 +116,16 @@ def safe_step_ex(mode, x, aux, step, u, gamma_b, hazards=None, mean=None, sigma=
 
 def max_threads():
     return lib().oracle_max_threads()
+
+
+def cars_cascade_loop(noise, steps=300, gamma_b=20.0):
+    """BASELINE config 1 (envs/simulated_cars_env.py:161-228): the hand
+    controller + CascadeCBFLayer.get_u_safe + env.step closed loop of one
+    SimulatedCars env from reset with velocity noise `noise`, in C (one
+    thread).  Returns (u_nom (steps,), u_safe (steps,), states (steps+1, 10))."""
+    un, us = np.zeros(steps), np.zeros(steps)
+    xs = np.zeros((steps + 1, 10))
+    rc = lib().oracle_cars_cascade_loop(float(noise), int(steps), float(gamma_b), _p(un), _p(us), _p(xs))
+    if rc:
+        raise RuntimeError(f"oracle_cars_cascade_loop: no QP solution at step {rc - 1}")
+    return un, us, xs

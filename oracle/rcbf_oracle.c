@@ -128,16 +128,25 @@ static int qp_exact_as(int m, int n, const double* Pd, float Gf[][MAXN], const f
 static int qp_exact(int m, int n, const double* Pd, float Gf[][MAXN], const float* hf, double* z) {
     return qp_exact_as(m, n, Pd, Gf, hf, z, NULL, NULL, NULL);
 }
+static int qp_exact_as_d(int m, int n, const double* Pd, double G[][MAXN], const double* h, double* z, int* S_out,
+                         int* k_out, double* lam_out);
 static int qp_exact_as(int m, int n, const double* Pd, float Gf[][MAXN], const float* hf, double* z, int* S_out,
                        int* k_out, double* lam_out) {
-    double G[MAXM][MAXN], h[MAXM], scale = 1.0, ah = 0.0, ag = 0.0;
+    double G[MAXM][MAXN], h[MAXM];
     for (int r = 0; r < m; ++r) {
         h[r] = hf[r];
+        for (int k = 0; k < n; ++k) G[r][k] = Gf[r][k];
+    }
+    return qp_exact_as_d(m, n, Pd, G, h, z, S_out, k_out, lam_out);
+}
+/* the same on fp64 rows (the Cascade layer's, cbf_qp.py:55-286) */
+static int qp_exact_as_d(int m, int n, const double* Pd, double G[][MAXN], const double* h, double* z, int* S_out,
+                         int* k_out, double* lam_out) {
+    double scale = 1.0, ah = 0.0, ag = 0.0;
+    for (int r = 0; r < m; ++r) {
         if (fabs(h[r]) > ah) ah = fabs(h[r]);
-        for (int k = 0; k < n; ++k) {
-            G[r][k] = Gf[r][k];
+        for (int k = 0; k < n; ++k)
             if (fabs(G[r][k]) > ag) ag = fabs(G[r][k]);
-        }
     }
     scale += ah + ag;
     const double tol = 1e-10 * scale;
@@ -235,6 +244,27 @@ static int qp_exact_as(int m, int n, const double* Pd, float Gf[][MAXN], const f
 }
 
 /* ----------------------------------------------------------------- envs */
+/* SimulatedCarsEnv.step's physics (envs/simulated_cars_env.py:55-77) for an fp64 action */
+static void cars_physics(double* x, double* t, int32_t* step, double a) {
+    double vdes0 = 30.0 - 10.0 * sin(0.2 * (*t));
+    double acc[5];
+    acc[0] = 4.0 * (vdes0 - x[1]);
+    for (int i = 1; i < 5; ++i) acc[i] = 4.0 * (30.0 - x[2 * i + 1]);
+    double d01 = x[0] - x[2], d12 = x[2] - x[4], d24 = x[4] - x[8];
+    acc[1] += (-20.0 * d01) * (d01 < 6.0 ? 1.0 : 0.0);
+    acc[2] += (-20.0 * d12) * (d12 < 6.0 ? 1.0 : 0.0);
+    acc[4] += (-20.0 * d24) * (d24 < 13.0 ? 1.0 : 0.0);
+    for (int i = 0; i < 5; ++i) acc[i] *= 1.1;
+    double gu = 50.0 * a, v[5];
+    for (int i = 0; i < 5; ++i) v[i] = x[2 * i + 1];
+    for (int i = 0; i < 5; ++i) {
+        x[2 * i] += 0.02 * (v[i] + 0.0);
+        x[2 * i + 1] += 0.02 * (acc[i] + (i == 3 ? gu : 0.0));
+    }
+    *t = *t + 0.02;
+    *step += 1;
+}
+
 static void cars_env(double* x, double* t, int32_t* step, float a, float* rew, float* cost, uint8_t* done) {
     double vdes0 = 30.0 - 10.0 * sin(0.2 * (*t));
     double acc[5];
@@ -559,4 +589,65 @@ int oracle_max_threads(void) {
 #else
     return 1;
 #endif
+}
+
+/* ------------------------------------------------ config 1: the Cascade closed loop */
+/* BASELINE.json config 1, the reference's own demo (envs/simulated_cars_env.py:161-228): one SimulatedCars
+ * env from reset (positions 34, 28, 22, 16, 10; velocities 30 + noise, car 3 at 35; :108-125) for `steps`
+ * steps of
+ *   obs = x / [100, 30] (:143-158) -> state = obs * [100, 30] (DynamicsModel.get_state, dynamics.py:190-232,
+ *   fp64) -> the hand controller (:195-199) -> CascadeCBFLayer.get_u_safe (cbf_qp.py:29-53: the cars rows
+ *   of :149-219 + :224-238 with no robust term and gamma_b, P = diag(0.1, 10), q = 0; rows normalised by
+ *   max(|G_r|, |h_r|) as :270-273; the exact QP that quadprog returns at :276) -> env.step(u_nom + u_safe).
+ * u_nom_out, u_safe_out (steps,), x_out ((steps + 1) x 10): [nullable].  Returns 0, or 1 + the step whose
+ * QP had no solution. */
+int oracle_cars_cascade_loop(double noise, int steps, double gamma_b, double* u_nom_out, double* u_safe_out,
+                             double* x_out) {
+    double x[10] = {34.0, 30.0 + noise, 28.0, 30.0 + noise, 22.0, 30.0 + noise, 16.0, 35.0, 10.0, 30.0 + noise};
+    double t = 0.0;
+    int32_t st = 0;
+    if (x_out) memcpy(x_out, x, sizeof x);
+    for (int k = 0; k < steps; ++k) {
+        double s[10];
+        for (int i = 0; i < 10; ++i) {
+            const double o = (i & 1) ? x[i] / 30.0 : x[i] / 100.0;
+            s[i] = (i & 1) ? o * 30.0 : o * 100.0;
+        }
+        double u = (s[4] - s[6] - 0.4) * ((s[4] - s[6] - 0.4) < 0 ? 1.0 : 0.0);
+        u += (s[8] - s[6] + 0.4) * ((s[8] - s[6] + 0.4) > 0 ? 1.0 : 0.0);
+        /* Cascade rows (fp64) */
+        double p[5], v[5], a[5];
+        for (int i = 0; i < 5; ++i) { p[i] = s[2 * i]; v[i] = s[2 * i + 1]; a[i] = 4.0 * (30.0 - v[i]); }
+        const double d01 = p[0] - p[1], d12 = p[1] - p[2], d24 = p[2] - p[4];
+        a[1] = a[1] - 20.0 * d01 * (d01 < 6.0 ? 1.0 : 0.0);
+        a[2] = a[2] - 20.0 * d12 * (d12 < 6.0 ? 1.0 : 0.0);
+        a[3] = 0.0;
+        a[4] = a[4] - 20.0 * d24 * (d24 < 13.0 ? 1.0 : 0.0);
+        const double h13 = 0.5 * ((p[2] - p[3]) * (p[2] - p[3]) - 3.5 * 3.5);
+        const double h15 = 0.5 * ((p[4] - p[3]) * (p[4] - p[3]) - 3.5 * 3.5);
+        const double h13d = (p[3] - p[2]) * (v[3] - v[2]), h15d = (p[3] - p[4]) * (v[3] - v[4]);
+        const double Lff13 = (v[2] - v[3]) * v[2] + (p[2] - p[3]) * a[2] + (v[3] - v[2]) * v[3] + (p[3] - p[2]) * a[3];
+        const double Lff15 = (v[3] - v[4]) * v[3] + (p[3] - p[4]) * a[3] + (v[4] - v[3]) * v[4] + (p[4] - p[3]) * a[4];
+        const double Lg13 = 50.0 * (p[3] - p[2]), Lg15 = 50.0 * (p[3] - p[4]);
+        double G[MAXM][MAXN] = {{0}}, h[MAXM];
+        h[0] = Lff13 + (gamma_b + gamma_b) * h13d + gamma_b * gamma_b * h13 + Lg13 * u;
+        h[1] = Lff15 + (gamma_b + gamma_b) * h15d + gamma_b * gamma_b * h15 + Lg15 * u;
+        G[0][0] = -Lg13; G[1][0] = -Lg15; G[0][1] = G[1][1] = -2e2;
+        G[2][0] = 1.0; h[2] = 10.0 - u;
+        G[3][0] = -1.0; h[3] = 10.0 + u;
+        for (int r = 0; r < 4; ++r) { /* cbf_qp.py:270-273 */
+            double nr = fabs(h[r]);
+            for (int c = 0; c < 2; ++c) if (fabs(G[r][c]) > nr) nr = fabs(G[r][c]);
+            for (int c = 0; c < 2; ++c) G[r][c] = G[r][c] / nr;
+            h[r] = h[r] / nr;
+        }
+        const double Pd[2] = {0.1, 1e1};
+        double z[MAXN];
+        if (qp_exact_as_d(4, 2, Pd, G, h, z, NULL, NULL, NULL)) return k + 1;
+        if (u_nom_out) u_nom_out[k] = u;
+        if (u_safe_out) u_safe_out[k] = z[0];
+        cars_physics(x, &t, &st, u + z[0]);
+        if (x_out) memcpy(x_out + 10 * (k + 1), x, sizeof x);
+    }
+    return 0;
 }

@@ -101,6 +101,7 @@ SIGNATURES = {
     "rcbf_obs_safe_action_jac": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "rcbf_safe_action_apply_jac": [_I64, _I32, _P, _P, _P, _P],
     "rcbf_cascade_u_safe": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "rcbf_cascade_u_safe_sync": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_uint32, _P],
     "rcbf_env_reset": [_PRM, _I64, _P, _P, _U64, _I64, _P, _P, _P, _P, _P, _P],
     "rcbf_env_step": [_PRM, _I64, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],
     "rcbf_safe_step": [_PRM, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _U64, _I64, _P],

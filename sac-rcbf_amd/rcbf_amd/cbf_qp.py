@@ -8,6 +8,7 @@ its slack-violation warning (:283-284) is: any row whose slack |epsilon|
 exceeds 0.1 prints the reference's message (get_u_safe and solve_qp).
 """
 import ctypes
+import weakref
 
 import numpy as np
 import torch
@@ -15,6 +16,9 @@ import torch
 from . import _lib
 from .dynamics import DYNAMICS_MODE
 from .params import make_params
+
+
+_SYNC_MAX_B = 256  # rcbf_cascade_u_safe_sync: one workgroup
 
 
 def _warn_slack(eps):
@@ -39,11 +43,18 @@ class CascadeCBFLayer:
         _lib.load()
 
     def get_u_safe(self, u_nom, s, mean_pred, sigma):
-        """cbf_qp.py:29-53: u_safe such that env.step(u_nom + u_safe) is safe."""
+        """cbf_qp.py:29-53: u_safe such that env.step(u_nom + u_safe) is safe.
+        Up to 256 samples (the reference's loop calls it on one): the inputs
+        go into a pinned host block the kernel reads in place and the call
+        returns on its completion word (rcbf_cascade_u_safe_sync) -- no copy
+        and no stream synchronisation; larger batches go through device
+        tensors (rcbf_cascade_u_safe)."""
         if not torch.cuda.is_available():
             raise RuntimeError("CascadeCBFLayer needs a HIP device (MI355X); there is no CPU fallback")
         un = np.asarray(u_nom, np.float64)
         single = un.ndim == 1
+        if np.atleast_2d(un).shape[0] <= _SYNC_MAX_B:
+            return self._get_u_safe_sync(un, s, mean_pred, sigma, single)
         dev = torch.device("cuda", torch.cuda.current_device())
 
         def d(a):
@@ -64,6 +75,56 @@ class CascadeCBFLayer:
         self.last_eps = eps.cpu().numpy()
         _warn_slack(self.last_eps)
         return res[0] if single else res
+
+    def _get_u_safe_sync(self, un, s, mean_pred, sigma, single):
+        U = np.atleast_2d(un)
+        X = np.atleast_2d(np.asarray(s, np.float64))
+        B, n_u = U.shape
+        n_s = X.shape[1]
+        st = self._staging(B, n_s, n_u)
+        st["u"][:B * n_u] = U.reshape(-1)
+        st["x"][:B * n_s] = X.reshape(-1)
+        st["m"][:B * n_s] = np.atleast_2d(np.asarray(mean_pred, np.float64)).reshape(-1)
+        st["s"][:B * n_s] = np.atleast_2d(np.asarray(sigma, np.float64)).reshape(-1)
+        st["seq"] = (st["seq"] + 1) & 0xFFFFFFFF or 1
+        dev = torch.cuda.current_device()
+        rc = _lib.load().rcbf_cascade_u_safe_sync(ctypes.byref(self._prm), B, st["pu"], st["px"], st["pm"], st["ps"],
+                                                  st["po"], st["pst"], st["pe"], st["pw"], st["seq"],
+                                                  _lib.stream_of(dev))
+        _lib.check(rc, "rcbf_cascade_u_safe_sync")
+        if (st["status"][:B] != _lib.QP_OK).any():
+            raise ValueError("constraints are inconsistent, no solution")  # quadprog's ValueError (:279-281)
+        res = st["o"][:B * n_u].reshape(B, n_u).copy()
+        self.last_eps = st["e"][:B].copy()
+        _warn_slack(self.last_eps)
+        return res[0] if single else res
+
+    def _staging(self, B, n_s, n_u):
+        """A pinned host block (rcbf_host_alloc) of _SYNC_MAX_B samples: u_nom,
+        state, mean, sigma, u_safe, epsilon (f64), status (i32), the completion
+        word; numpy views over it."""
+        st = self.__dict__.get("_stage")
+        if st is not None:
+            return st
+        cap = _SYNC_MAX_B
+        sizes = [("u", cap * n_u * 8), ("x", cap * n_s * 8), ("m", cap * n_s * 8), ("s", cap * n_s * 8),
+                 ("o", cap * n_u * 8), ("e", cap * 8), ("status", cap * 4), ("w", 64)]
+        total = sum(-(-b // 64) * 64 for _, b in sizes)
+        ptr = ctypes.c_void_p()
+        _lib.check(_lib.load().rcbf_host_alloc(total, ctypes.byref(ptr)), "rcbf_host_alloc")
+        st, off = {"base": ptr.value, "seq": 0}, 0
+        for name, b in sizes:
+            a = ptr.value + off
+            st["p" + ("st" if name == "status" else name)] = a
+            if name == "status":
+                st[name] = np.ctypeslib.as_array((ctypes.c_int32 * cap).from_address(a))
+            elif name != "w":
+                st[name] = np.ctypeslib.as_array((ctypes.c_double * (b // 8)).from_address(a))
+            off += -(-b // 64) * 64
+        ctypes.c_uint32.from_address(st["pw"]).value = 0
+        self._stage = st
+        self._stage_fin = weakref.finalize(self, _lib.load().rcbf_host_free, ptr.value)
+        return st
 
     def get_cbf_qp_constraints(self, u_nom, state, mean_pred, sigma_pred):
         """cbf_qp.py:55-240 (fp64), single sample or batch."""

@@ -77,6 +77,12 @@ for step in "$@"; do
     benchx) run benchx 600 python bench.py --extra --no-cpu-baseline ;;
     aqltest) run aqltest 300 python -u -m pytest tests/test_gpu_aql.py -q -rf --timeout 200 --timeout-method thread ;;
     aqltl) run aqltl 300 python -u scripts/exp_aql_timeline.py ;;
+    scal)  # per-shard batches for the 1 -> 8 projection (scripts/scaling_projection.py), both command forms
+      for b in 65536 32768 16384 8192; do
+        run "scal_d_$b" 200 python bench.py --no-cpu-baseline --no-span --batch "$b" --steps 20 --warmup 5
+        run "scal_l_$b" 200 python bench.py --no-cpu-baseline --no-span --batch "$b"
+      done
+      python scripts/scaling_projection.py "$OUT/scaling_projection_$TAG.json" "$OUT"/scal_*.log > /dev/null ;;
     drvaql) run drvaql 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --launch aql ;;
     benchaql) run benchaql 300 python bench.py --no-cpu-baseline --launch aql ;;
     sweep)  # waves per SIMD: B = 32768 (half the SIMDs), 65536 (one wave each), 98304, 131072 (two)

@@ -24,7 +24,7 @@ def _args(*argv):
 
 
 @pytest.mark.parametrize("cfg,env,batch,workload,scaling", [
-    (0, "SimulatedCars", 65536, "step", "weak"), (1, "SimulatedCars", 1, "step", "weak"),
+    (0, "SimulatedCars", 65536, "step", "weak"), (1, "SimulatedCars", 1, "closed_loop", "weak"),
     (2, "SimulatedCars", 4096, "step", "weak"), (3, "Unicycle", 4096, "step", "weak"),
     (4, "SimulatedCars", 262144, "step", "strong"), (5, "SimulatedCars", 4096, "sac_update", "weak")])
 def test_config_presets_follow_baseline_json(cfg, env, batch, workload, scaling):

@@ -107,3 +107,14 @@ def test_c_oracle_gradient_matches_reference_fixtures(golden, name, mode, tag):
     g_np, _ = O.safe_action_diff_grad(mode, x[:300], u[:300], mu[:300], sg[:300], float(d["gamma_b"]), w[:300],
                                       hazards=hz)
     assert rel(grad[:300], g_np) <= 1e-9
+
+
+def test_c_closed_loop_config1_matches_the_reference_loop(golden):
+    """BASELINE config 1 in C (oracle_cars_cascade_loop, bench.py --config 1's
+    CPU baseline): the hand controller, the Cascade QP and the env over the
+    golden 300-step episode equal the reference's own closed loop."""
+    cl = golden("closed_loop_cars")
+    un, us, xs = C.cars_cascade_loop(float(cl["noise"]), 300)
+    assert np.max(np.abs(un - cl["u_nom"][:, 0]) / np.maximum(1, np.abs(cl["u_nom"][:, 0]))) <= 1e-12
+    assert np.max(np.abs(us - cl["u_safe"][:, 0]) / np.maximum(1, np.abs(cl["u_safe"][:, 0]))) <= 1e-7
+    assert np.max(np.abs(xs - cl["state"]) / np.maximum(1, np.abs(cl["state"]))) <= 1e-9
