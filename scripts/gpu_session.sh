@@ -145,6 +145,13 @@ for step in "$@"; do
     gpt)    run gpt 600 python -u -m pytest tests/test_gpu_gp.py tests/test_gpu_parity.py -q -rf --timeout 300 --timeout-method thread ;;
     loop)   run loop 900 python -u -m pytest tests/test_gpu_training_loop.py -q -rf -s --timeout 600 --timeout-method thread ;;
     gpgb)   run gpgb 300 python -u scripts/gp_graph_bench.py ;;
+    gpsk)   # split-K count sweep of the B = 256 GP posterior (study build build/variants/librcbf_gpsplit.so)
+      for sk in 0 6 11 16 22 32 47; do
+        if [ "$sk" = 0 ]; then e=""; else e="RCBF_GP_SPLIT=$sk"; fi
+        env $e RCBF_HIP_LIB=build/variants/librcbf_gpsplit.so GP_BENCH_ONLY=love100:256 timeout -k 10 200 \
+          python scripts/gp_graph_bench.py 20 5 > "$OUT/gpsk_$sk.log" 2>&1 || exit 1
+        echo "sk=$sk $(tail -1 "$OUT/gpsk_$sk.log")" >> "$OUT/gpsk_sum.txt"
+      done ;;
     single) run single 300 python -u scripts/single_env_latency.py ;;
     msab)   # model step / predict_next_state: product vs build/variants/librcbf_modelold.so, 3 rounds
       for r in 1 2 3; do for n in prod modelold; do
