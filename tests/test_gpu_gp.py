@@ -359,6 +359,35 @@ def test_gp_gemv_poisoned_counter_is_detected_and_reset(rank):
         assert torch.equal(m1, m2) and torch.equal(s1, s2)
 
 
+def test_gp_workspace_per_stream():
+    """GEMV calls on two streams at once use two
+    workspaces (GPDisturbanceModel._workspace keys them by stream), so their
+    arrival counters never meet: 64 interleaved B = 1 calls on two streams,
+    no GPU-side sync between them, each bit-equal to the same query on the
+    default stream, and no fail word set."""
+    from rcbf_amd import gp
+    rng = np.random.default_rng(9)
+    tx, ty = _data(rng, 1500, 10)
+    hyper = [(rng.uniform(0.8, 2.5), rng.uniform(0.05, 0.5), rng.uniform(0.01, 0.2)) for _ in range(10)]
+    model = gp.GPDisturbanceModel(tx, ty, hyper, rank=100)
+    q = torch.as_tensor((rng.normal(0, 1, (64, 10)) * tx.std(0)).astype(np.float32), device="cuda")
+    want = [model.predict(q[j:j + 1].contiguous()) for j in range(64)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream())
+    got = []
+    for j in range(64):
+        with torch.cuda.stream(streams[j % 2]):
+            got.append(model.predict(q[j:j + 1].contiguous()))
+    torch.cuda.synchronize()
+    keys = {k for k in model._ws}
+    assert len(keys) == 3  # the default stream's and one per side stream
+    for (m1, s1), (m2, s2) in zip(want, got):
+        assert torch.equal(m1, m2) and torch.equal(s1, s2)
+    model.check_failures()
+
+
 def test_state_from_obs_kernel_matches_reference_get_state(golden):
     """DynamicsModel.get_state on device fp32 observations is one launch
     (rcbf_state_from_obs); it returns the reference's own torch get_state
