@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "rcbf_device.hpp"
 
@@ -129,6 +130,152 @@ __device__ __forceinline__ void st_out2(float* p, float a, float b) {
     w.f[0] = a;
     w.f[1] = b;
     st_out<uint64_t>(reinterpret_cast<uint64_t*>(p), w.u);
+}
+
+// ---------------------------------------------------------------------------
+// STUDY BUILD (-DRCBF_WT_OUT=1, scripts/exp_wt_nofence.py; the product is
+// RCBF_WT_OUT=0 and its machine code is unchanged by this block).  Measured
+// r06l (profiles/r06/wt_nofence_r06l.txt): the write-through stores cost the
+// cars step 1.35 us of in-kernel span (2.56 -> 3.91) to save 0.4-0.7 us of
+// boundary, so 3.88 -> 4.56-4.63 us per step; not adopted.
+// Write-through outputs of the fused step (RCBF_WT_OUT).  Every byte the step
+// writes leaves the XCD's L2 as it is stored (`sc1`), and each wave waits for
+// its stores before it ends, so when the dispatch completes nothing it wrote is
+// dirty in any L2: the next step (an AQL packet with an agent-scope acquire and
+// NO release, csrc/rcbf_aql.hip) reads it from the coherent side on whichever
+// XCD it runs, and two XCDs never hold dirty copies of one output line.  The
+// per-step L2 write-back of the kernel-end release is what it removes
+// (DESIGN §3.5).  Narrow `sc1` stores are one fabric write per lane, so the
+// per-env scalars of a full wave are staged in LDS and leave as 16-B chunks
+// (WtStage).
+// ---------------------------------------------------------------------------
+#ifndef RCBF_WT_OUT
+#define RCBF_WT_OUT 0
+#endif
+
+// 16-byte write-through store of two doubles (a state pair)
+__device__ __forceinline__ void st_wt2d(double* p, double a, double b) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2 w = {a, b};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+}
+
+// one lane's write-through store of a 1/4/8-byte value (partial waves, rare stores)
+template <typename T>
+__device__ __forceinline__ void st_wt(T* p, T v) {
+    static_assert(sizeof(T) == 1 || sizeof(T) == 4 || sizeof(T) == 8, "st_wt: 1, 4 or 8 bytes");
+    using U = typename std::conditional<sizeof(T) == 1, uint8_t,
+                                        typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type>::type;
+    U u;
+    __builtin_memcpy(&u, &v, sizeof(T));
+    __hip_atomic_store(reinterpret_cast<U*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the store flavour of one output: write-through under WT, `nt` otherwise
+template <bool WT, typename T>
+__device__ __forceinline__ void st_any(T* p, T v) {
+    if constexpr (WT)
+        st_wt(p, v);
+    else
+        st_out(p, v);
+}
+template <bool WT>
+__device__ __forceinline__ void st_any2d(double* p, double a, double b) {
+    if constexpr (WT)
+        st_wt2d(p, a, b);
+    else
+        st_out2d(p, a, b);
+}
+
+// Staged write-through of a full wave's per-env scalars.  Segment s holds one
+// SZ_s-byte value per lane; the wave's 64 values of a segment are one
+// contiguous (64 SZ_s)-byte block at dst_s (= array + first env of the wave x
+// SZ_s), i.e. 4 SZ_s chunks of 16 B.  The LDS block mirrors the chunk order
+// (segment s at byte 16 pre_s), so chunk c is read from lds + 16 c and goes to
+// dst_s + 16 (c - pre_s), the chunks of every segment dealt over the lanes
+// together: a handful of dwordx4 `sc1` stores per wave instead of one narrow
+// fabric write per lane and output.
+template <int... SZ>
+struct WtStage {
+    static constexpr int kN = sizeof...(SZ);
+    static constexpr int kSz[kN] = {SZ...};
+    static constexpr int pre(int s) {
+        int p = 0;
+        for (int j = 0; j < s; ++j) p += 4 * kSz[j];
+        return p;
+    }
+    static constexpr int kChunks = pre(kN);
+    static constexpr int kBytes = 16 * kChunks;
+    // lane deposits its value of segment S
+    template <int S, typename T>
+    static __device__ __forceinline__ void put(char* lds, int lane, T v) {
+        static_assert(sizeof(T) == kSz[S], "WtStage::put: value size");
+        *reinterpret_cast<T*>(lds + 16 * pre(S) + lane * (int)sizeof(T)) = v;
+    }
+    // the wave's chunks to HBM (all lanes of the wave call it)
+    static __device__ __forceinline__ void flush(const char* lds, int lane, char* const (&dst)[kN]) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_wave_barrier();
+        constexpr int NJ = (kChunks + 63) / 64;
+        f4 v[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int c = j * 64 + lane;
+            if (kChunks % 64 == 0 || c < kChunks) v[j] = reinterpret_cast<const f4*>(lds)[c];
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int c = j * 64 + lane;
+            if (kChunks % 64 == 0 || c < kChunks) {
+                char* d = nullptr;
+#pragma unroll
+                for (int s = 0; s < kN; ++s)
+                    if (c >= pre(s) && c < pre(s + 1)) d = dst[s] + 16 * (c - pre(s));
+                asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(d), "v"(v[j]) : "memory");
+            }
+        }
+    }
+    // true when every segment's block of this wave is 16-B aligned
+    static __device__ __forceinline__ bool aligned(char* const (&dst)[kN]) {
+        uintptr_t a = 0;
+#pragma unroll
+        for (int s = 0; s < kN; ++s) a |= reinterpret_cast<uintptr_t>(dst[s]);
+        return (a & 15) == 0;
+    }
+    // The whole store: val[s] holds this lane's value of segment s in its low
+    // SZ_s bytes; dst[s] = the segment's array + the wave's first env x SZ_s.
+    // full: all 64 lanes of the wave are live (wave-uniform); otherwise, or
+    // when a block is unaligned, every lane stores its own values write-through.
+    static __device__ __forceinline__ void store(char* lds, int lane, bool full, char* const (&dst)[kN],
+                                                 const uint64_t (&val)[kN]) {
+        if (full && aligned(dst)) {
+#pragma unroll
+            for (int s = 0; s < kN; ++s) {
+                char* q = lds + 16 * pre(s) + lane * kSz[s];
+                if (kSz[s] == 8) *reinterpret_cast<uint64_t*>(q) = val[s];
+                else if (kSz[s] == 4) *reinterpret_cast<uint32_t*>(q) = (uint32_t)val[s];
+                else *reinterpret_cast<uint8_t*>(q) = (uint8_t)val[s];
+            }
+            flush(lds, lane, dst);
+        } else {
+#pragma unroll
+            for (int s = 0; s < kN; ++s) {
+                char* q = dst[s] + lane * kSz[s];
+                if (kSz[s] == 8) st_wt(reinterpret_cast<uint64_t*>(q), val[s]);
+                else if (kSz[s] == 4) st_wt(reinterpret_cast<uint32_t*>(q), (uint32_t)val[s]);
+                else st_wt(reinterpret_cast<uint8_t*>(q), (uint8_t)val[s]);
+            }
+        }
+    }
+};
+
+// the low bytes of a value as a WtStage::store operand
+template <typename T>
+__device__ __forceinline__ uint64_t wt_bits(T v) {
+    static_assert(sizeof(T) <= 8 && !std::is_pointer<T>::value, "wt_bits: a scalar value");
+    uint64_t u = 0;
+    __builtin_memcpy(&u, &v, sizeof(T));
+    return u;
 }
 
 // Phase timestamps of the fused step for the study build only
@@ -383,7 +530,7 @@ __device__ __forceinline__ void state_from_env(const double* xs, float* s32) {
 // The episode counter is only touched when the env resets.
 // obs_cache (unicycle): cos/sin/goal distance of the post-step state, valid
 // unless the env was reset (then obs_cache[3] = 0 and the obs is recomputed).
-template <int SOLVER, int MODE, int K, bool ST = false>
+template <int SOLVER, int MODE, int K, bool ST = false, bool WT = false>
 __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i, double* xs, double& a, int& st,
                                               uint32_t* episode, const float* us, const float* m, const float* s,
                                               float* uf, float& rew, float& cst, bool& dn, bool& gm, int& status,
@@ -436,7 +583,12 @@ __device__ __forceinline__ void safe_step_one(const rcbf_params& prm, int64_t i,
     if (auto_reset && dn) {
         // ep_pre: the caller loaded episode[i] with the state (reset_foreseeable)
         uint32_t ep = episode ? (ep_pre ? ep0 : episode[i]) + 1u : 0u;
-        if (episode) episode[i] = ep;
+        if (episode) {
+            if constexpr (WT)
+                st_wt(&episode[i], ep);
+            else
+                episode[i] = ep;
+        }
         env_reset_one<MODE>(nullptr, i, seed, off, ep, xs, a, st);
         if (obs_cache) {
             if constexpr (MODE == RCBF_MODE_UNICYCLE) {  // the reset state's obs inputs

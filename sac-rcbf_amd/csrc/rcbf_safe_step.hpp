@@ -64,7 +64,7 @@ __device__ __forceinline__ void store_state(double* x, int64_t B, int64_t i, con
     if constexpr (NS % 2) st_out(&x[(NS - 1) * B + i], xs[NS - 1]);
 }
 
-template <int MODE>
+template <int MODE, bool WT = false>
 __device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double* xs,
                                             const double* obs_cache = nullptr) {
     constexpr int NO = Dims<MODE, 1>::NO;
@@ -80,10 +80,19 @@ __device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double*
     if constexpr (MODE == RCBF_MODE_SIMULATED_CARS) {
         float* ov = obs + i * NO;  // 40 B rows, 8 B aligned
 #pragma unroll
-        for (int k = 0; k < NO / 2; ++k) st_out2(ov + 2 * k, (float)o[2 * k], (float)o[2 * k + 1]);
+        for (int k = 0; k < NO / 2; ++k) {
+            if constexpr (WT) {
+                const float pr[2] = {(float)o[2 * k], (float)o[2 * k + 1]};
+                uint64_t w;
+                __builtin_memcpy(&w, pr, 8);
+                st_wt(reinterpret_cast<uint64_t*>(ov + 2 * k), w);
+            } else {
+                st_out2(ov + 2 * k, (float)o[2 * k], (float)o[2 * k + 1]);
+            }
+        }
     } else {
 #pragma unroll
-        for (int k = 0; k < NO; ++k) st_out(&obs[i * NO + k], (float)o[k]);
+        for (int k = 0; k < NO; ++k) st_any<WT>(&obs[i * NO + k], (float)o[k]);
     }
 }
 
@@ -92,7 +101,7 @@ __device__ __forceinline__ void store_obs32(float* obs, int64_t i, const double*
 // stored: the write-through store is an asm with a memory clobber, which
 // would otherwise hold each following LDS read (and its wait) behind the
 // previous store.
-template <int MODE>
+template <int MODE, bool WT = false>
 __device__ __forceinline__ void store_obs_chunks(float* obs, int64_t base, const float* lds_wave) {
     constexpr int NO = Dims<MODE, 1>::NO;
     const int lane = threadIdx.x & 63;
@@ -110,7 +119,7 @@ __device__ __forceinline__ void store_obs_chunks(float* obs, int64_t base, const
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int c = j * 64 + lane;
-        if (CH % 64 == 0 || c < CH) st_out4<MODE == RCBF_MODE_SIMULATED_CARS>(dst + 4 * c, chunk[j]);
+        if (CH % 64 == 0 || c < CH) st_out4<WT || MODE == RCBF_MODE_SIMULATED_CARS>(dst + 4 * c, chunk[j]);
     }
 }
 
@@ -119,7 +128,7 @@ __device__ __forceinline__ void store_obs_chunks(float* obs, int64_t base, const
 // store the block as 16-byte chunks, chunk c by lane c%64 -- every store
 // instruction covers whole contiguous lines (cars: 3 dwordx4 instead of 5
 // strided dwordx2).  Partial or unaligned waves take the per-lane path.
-template <int MODE>
+template <int MODE, bool WT = false>
 __device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_t B, const double* xs,
                                                    const double* obs_cache, float* lds_wave) {
     constexpr int NO = Dims<MODE, 1>::NO;
@@ -131,7 +140,7 @@ __device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_
     const bool full = (base + 64 <= B) && ((reinterpret_cast<uintptr_t>(obs) & 15) == 0);
 #endif
     if (!full) {
-        store_obs32<MODE>(obs, i, xs, obs_cache);
+        store_obs32<MODE, WT>(obs, i, xs, obs_cache);
         return;
     }
     double o[NO];
@@ -151,7 +160,7 @@ __device__ __forceinline__ void store_obs32_staged(float* obs, int64_t i, int64_
 #pragma unroll
         for (int k = 0; k < NO; ++k) lds_wave[lane * NO + k] = (float)o[k];
     }
-    store_obs_chunks<MODE>(obs, base, lds_wave);
+    store_obs_chunks<MODE, WT>(obs, base, lds_wave);
 }
 
 // The fused safe step (rcbf_safe_step): one env per lane.  ST = true only in
@@ -179,8 +188,19 @@ __global__ void __launch_bounds__(BS) k_safe_step(int64_t B, double* __restrict_
                                                       int auto_reset, uint64_t seed, int64_t off, rcbf_params prm,
                                                       int prior_cols = 0, unsigned long long* stamp_buf = nullptr) {
     using D = Dims<MODE, K>;
+    // RCBF_WT_OUT: every output write-through, the wave's stores drained before
+    // it ends (rcbf_common.hpp, WtStage); the study stamps build keeps the nt form
+    constexpr bool WT = RCBF_WT_OUT != 0 && !ST;
     int64_t i = env_index<BS>();
     if (i >= B) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t wbase = i - lane;
+    const bool wfull = wbase + 64 <= B;  // wave-uniform: every lane of this wave is live
+    constexpr int kWtBytes = WT ? 16 * 160 : 16;  // per wave: the largest WtStage below (unicycle, 152 chunks)
+    __shared__ __attribute__((aligned(16))) char wt_lds_all[BS / 64][kWtBytes];
+    char* wt_lds = wt_lds_all[threadIdx.x >> 6];
+    (void)wt_lds;
+    (void)wfull;
     unsigned long long span_t0 = 0, span_c0 = 0;
     if constexpr (SPAN) {
         span_t0 = __builtin_amdgcn_s_memrealtime();
@@ -265,14 +285,26 @@ __global__ void __launch_bounds__(BS) k_safe_step(int64_t B, double* __restrict_
         const bool rs = auto_reset && dn;
         if (rs) {
             const uint32_t ep = episode ? (ep_pre ? ep0 : episode[i]) + 1u : 0u;
-            if (episode) episode[i] = ep;
+            if (episode) {
+                if constexpr (WT)
+                    st_wt(&episode[i], ep);
+                else
+                    episode[i] = ep;
+            }
             env_reset_one<MODE>(nullptr, i, seed, off, ep, xs, a, st);
         }
 #pragma unroll
         for (int p = 0; p < D::NS / 2; ++p)
-            if (p != 3) st_out2d(&x[2 * (p * B + i)], xs[2 * p], xs[2 * p + 1]);
-        st_out(&aux[i], a);
-        st_out(&step[i], st);
+            if (p != 3) st_any2d<WT>(&x[2 * (p * B + i)], xs[2 * p], xs[2 * p + 1]);
+        if constexpr (WT) {
+            using E = WtStage<8, 4>;  // aux, step
+            char* const dst[2] = {reinterpret_cast<char*>(aux + wbase), reinterpret_cast<char*>(step + wbase)};
+            const uint64_t val[2] = {wt_bits(a), wt_bits(st)};
+            E::store(wt_lds, lane, wfull, dst, val);
+        } else {
+            st_out(&aux[i], a);
+            st_out(&step[i], st);
+        }
         __builtin_amdgcn_sched_barrier(0);  // keep the early stores ahead of the layer's chain
         if constexpr (kRowsFirst) {
             layer_solve_raw<MODE, K>(prm, us, uf, L);  // the same solve as layer_forward<..., RAW>
@@ -284,24 +316,81 @@ __global__ void __launch_bounds__(BS) k_safe_step(int64_t B, double* __restrict_
         cars_env_post<float>(xs, acc3, uf[0], o);  // car 3's velocity and the reward
         xs[7] = rs ? v3_reset : xs[7];
         rew = o.reward;
-        st_out2d(&x[2 * (3 * B + i)], xs[6], xs[7]);
+        st_any2d<WT>(&x[2 * (3 * B + i)], xs[6], xs[7]);
     } else {
-        safe_step_one<SOLVER, MODE, K, ST>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status,
-                                           auto_reset, seed, off, stamps, oc, ep_pre, ep0);
-        store_state<MODE>(x, B, i, xs);
-        st_out(&aux[i], a);
-        st_out(&step[i], st);
+        safe_step_one<SOLVER, MODE, K, ST, WT>(prm, i, xs, a, st, episode, us, m, s, uf, rew, cst, dn, gm, status,
+                                               auto_reset, seed, off, stamps, oc, ep_pre, ep0);
+        if constexpr (WT) {
+#pragma unroll
+            for (int p = 0; p < D::NS / 2; ++p) st_wt2d(&x[2 * (p * B + i)], xs[2 * p], xs[2 * p + 1]);
+            // the odd component (unicycle theta), aux and step leave with the outputs below
+        } else {
+            store_state<MODE>(x, B, i, xs);
+            st_out(&aux[i], a);
+            st_out(&step[i], st);
+        }
     }
     __shared__ float obs_stage[BS / 64][64 * D::NO];
-    store_obs32_staged<MODE>(obs_out, i, B, xs, oc, obs_stage[threadIdx.x >> 6]);
+    store_obs32_staged<MODE, WT>(obs_out, i, B, xs, oc, obs_stage[threadIdx.x >> 6]);
+    if constexpr (WT) {
+        constexpr int NU4 = 4 * D::NU;
+        float ufc[D::NU];
 #pragma unroll
-    for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
-    st_out(&reward[i], rew);
-    st_out(&cost[i], cst);
-    st_out(&done[i], (uint8_t)dn);
-    if (goal_met) st_out(&goal_met[i], (uint8_t)gm);
+        for (int c = 0; c < D::NU; ++c) ufc[c] = uf[c];
+        char* const u_d = reinterpret_cast<char*>(u_out + wbase * D::NU);
+        char* const r_d = reinterpret_cast<char*>(reward + wbase);
+        char* const c_d = reinterpret_cast<char*>(cost + wbase);
+        char* const d_d = reinterpret_cast<char*>(done + wbase);
+        uint64_t u_v = 0;
+        __builtin_memcpy(&u_v, ufc, sizeof(ufc));
+        const uint64_t r_v = wt_bits(rew), c_v = wt_bits(cst), d_v = (uint64_t)dn;
+        if constexpr (MODE == RCBF_MODE_SIMULATED_CARS && RCBF_EARLY_STORE) {
+            if (goal_met) {
+                using E = WtStage<NU4, 4, 4, 1, 1>;
+                char* const dst[5] = {u_d, r_d, c_d, d_d, reinterpret_cast<char*>(goal_met + wbase)};
+                const uint64_t val[5] = {u_v, r_v, c_v, d_v, (uint64_t)gm};
+                E::store(wt_lds, lane, wfull, dst, val);
+            } else {
+                using E = WtStage<NU4, 4, 4, 1>;
+                char* const dst[4] = {u_d, r_d, c_d, d_d};
+                const uint64_t val[4] = {u_v, r_v, c_v, d_v};
+                E::store(wt_lds, lane, wfull, dst, val);
+            }
+        } else {
+            static_assert(D::NS % 2 == 1, "the late write-through block carries the odd state component");
+            char* const x_d = reinterpret_cast<char*>(x + (D::NS - 1) * B + wbase);
+            char* const a_d = reinterpret_cast<char*>(aux + wbase);
+            char* const s_d = reinterpret_cast<char*>(step + wbase);
+            const uint64_t x_v = wt_bits(xs[D::NS - 1]), a_v = wt_bits(a), s_v = wt_bits(st);
+            if (goal_met) {
+                using E = WtStage<8, 8, 4, NU4, 4, 4, 1, 1>;
+                static_assert(E::kBytes <= kWtBytes, "wt_lds");
+                char* const dst[8] = {x_d, a_d, s_d, u_d, r_d, c_d, d_d, reinterpret_cast<char*>(goal_met + wbase)};
+                const uint64_t val[8] = {x_v, a_v, s_v, u_v, r_v, c_v, d_v, (uint64_t)gm};
+                E::store(wt_lds, lane, wfull, dst, val);
+            } else {
+                using E = WtStage<8, 8, 4, NU4, 4, 4, 1>;
+                char* const dst[7] = {x_d, a_d, s_d, u_d, r_d, c_d, d_d};
+                const uint64_t val[7] = {x_v, a_v, s_v, u_v, r_v, c_v, d_v};
+                E::store(wt_lds, lane, wfull, dst, val);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < D::NU; ++c) st_out(&u_out[i * D::NU + c], uf[c]);
+        st_out(&reward[i], rew);
+        st_out(&cost[i], cst);
+        st_out(&done[i], (uint8_t)dn);
+        if (goal_met) st_out(&goal_met[i], (uint8_t)gm);
+    }
     stamps.mark(6, false);
-    report(status, status_out, i, fail_flag);
+    if constexpr (WT) {
+        if (status_out) st_wt(&status_out[i], (int32_t)status);
+        if (status != RCBF_QP_OK && fail_flag) atomicOr(fail_flag, 1 << status);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing this wave wrote is in flight when it ends
+    } else {
+        report(status, status_out, i, fail_flag);
+    }
     stamps.mark(7, true);
     if constexpr (SPAN) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have landed

@@ -22,7 +22,7 @@ B = 256 query the MFMA path.
 Asserted: the reference's observable contract -- info['cost'] as the
 reference envs report it, the refit cadence, every safe action inside
 safe_action_space, no 'QP Failed to solve', finite losses and gradients.
-The per-env-step time is recorded (gpurun_out/training_loop_r05.json when
+The per-env-step time is recorded (gpurun_out/training_loop_r06.json when
 that directory exists) for DESIGN §5.5 against BASELINE.md's reference
 pre-solve path (1.21 ms cars / 0.45 ms unicycle per RCBF_SAC.get_safe_action
 at B = 1)."""
@@ -243,7 +243,7 @@ def _record(name, rec):
                    "B = 256 (two safe-action calls, one with the gradient through the CBF-QP) to its drained end",
            "episodes": rec["episodes"]}
     if os.path.isdir(out_dir):
-        path = os.path.join(out_dir, "training_loop_r05.json")
+        path = os.path.join(out_dir, "training_loop_r06.json")
         data = json.load(open(path)) if os.path.exists(path) else {}
         data[name] = row
         json.dump(data, open(path, "w"), indent=1)
