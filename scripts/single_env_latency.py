@@ -90,6 +90,31 @@ def main():
         out[f"{name}_gp_get_state_us"] = per_call_us(lambda: gdm.get_state(o2))
         out[f"{name}_gp_predict_us"] = per_call_us(lambda: gpm.predict(s2))
         out[f"{name}_to_host_us"] = per_call_us(lambda: u.cpu())
+        # the one-launch host-result call on the 300-point fits: Lanczos rank 16 (above), and the exact factor the
+        # training-loop test's DynamicsModel uses below 800 points (3 column blocks: one more hand-off level)
+        from rcbf_amd.sac_cbf import get_safe_action_host
+        out[f"{name}_gp300_rank16_one_launch_host_result_us"] = per_call_us(
+            lambda: get_safe_action_host(layer, ot, u, gdm))
+        from rcbf_amd import gp as _gp
+        g16 = gdm.disturb_estimators
+        gdm.disturb_estimators = _gp.GPDisturbanceModel(np.asarray(gdm.train_x), np.asarray(gdm.train_y),
+                                                        g16.hyper, rank=None)
+        if True:
+            out[f"{name}_gp300_exact_one_launch_host_result_us"] = per_call_us(
+                lambda: get_safe_action_host(layer, ot, u, gdm))
+
+            def gapped():  # the training loop's pattern: the host busy ~0.3 ms between calls
+                t_end = time.perf_counter() + 3e-4
+                while time.perf_counter() < t_end:
+                    pass
+                t0 = time.perf_counter()
+                get_safe_action_host(layer, ot, u, gdm)
+                return time.perf_counter() - t0
+            for _ in range(20):
+                gapped()
+            out[f"{name}_gp300_exact_one_launch_after_300us_idle_us"] = round(
+                float(np.median([gapped() for _ in range(400)])) * 1e6, 1)
+        gdm.disturb_estimators = g16
         # the reference's gp_model_size N = 3000 with LOVE rank 100, select_action's call
         # as ONE launch whose action lands in pinned host memory (get_safe_action_host) vs the three launches
         # + .cpu()

@@ -88,6 +88,23 @@ def test_aql_steps_equal_hip_launches(queue, mode, B, hazards, layout):
     plan.free()
 
 
+def test_plan_longer_than_the_ring(queue):
+    """K = 5 000 steps through the 4 096-packet ring: rcbf_aql_run feeds the
+    packets in as the packet processor frees slots; the result equals 5 000
+    HIP launches bit for bit."""
+    B, K = 512, 5000
+    (e1, l1), (e2, l2) = _pair("SimulatedCars", B)
+    pool = [(torch.rand(B, 1, device="cuda") * 2 - 1).contiguous() for _ in range(5)]
+    o1, o2 = e1.make_outputs(), e2.make_outputs()
+    plan = queue.safe_step_plan(e2, pool, l2, steps=K, outputs=o2)
+    plan.run()
+    e1.safe_step_seq(pool, l1, outputs=o1, steps=K)
+    torch.cuda.synchronize()
+    _assert_same(_snapshot(e1, o1), _snapshot(e2, o2))
+    assert int(e2.episode.min()) >= 16  # 5 000 steps: every env through >= 16 time-limit resets
+    plan.free()
+
+
 def test_profiled_plan_times_and_span(queue):
     B = 65536
     (e1, l1), (e2, l2) = _pair("SimulatedCars", B)
