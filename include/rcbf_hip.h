@@ -274,9 +274,12 @@ int rcbf_gp_workspace_init(const rcbf_gp_model* m, float* workspace, hipStream_t
  * arrival count proves the counter was not zero when its call started -- the
  * workspace was not zero-filled, a call was aborted part-way, or two calls
  * shared the workspace at once -- and sets the workspace's fail word; the
- * outputs of such a call are not valid.  Returns RCBF_E_GP_HANDOFF if the word
- * is set, after zeroing every counter and the word (the next call is clean);
- * 0 otherwise. */
+ * outputs of such a call are not valid.  A counter that started off by less
+ * than its arrival count lets an early workgroup take the "last" ticket; such a
+ * call leaves its counter non-zero once the stream has drained, which the check
+ * also reads as a failure.  Returns RCBF_E_GP_HANDOFF if the word is set or any
+ * counter is non-zero, after zeroing every counter and the word (the next call
+ * is clean); 0 otherwise. */
 int rcbf_gp_workspace_check(const rcbf_gp_model* m, float* workspace, hipStream_t stream);
 
 /* DynamicsModel.predict_disturbance(test_x) with fitted GPs (dynamics.py:
@@ -308,7 +311,10 @@ int rcbf_gp_predict(const rcbf_gp_model* m, int64_t B, const float* x, float* me
  * `seq` -- the action is then on the host, with no copy or stream
  * synchronisation (as rcbf_env_step_sync).  The workspace is the GP's
  * (rcbf_gp_workspace_floats(m, 1), zero-filled once).  RCBF_E_BAD_MODE for
- * another solver; RCBF_E_BAD_SHAPE for B != 1 or a model of another width. */
+ * another solver; RCBF_E_BAD_SHAPE for B != 1 or a model of another width;
+ * RCBF_E_GP_HANDOFF (done_word given) when the kernel completed without
+ * publishing: a hand-off counter was not zero at the start, so no result was
+ * formed (rcbf_gp_workspace_check then reports and zeroes the counters). */
 int rcbf_gp_obs_safe_action(const rcbf_params* prm, const rcbf_gp_model* m, int64_t B, const float* obs,
                             const float* u_rl, float* mean_out, float* std_out, float* u_out, float* u_host,
                             uint32_t* done_word, uint32_t seq, int32_t* status_out, int32_t* fail_flag,

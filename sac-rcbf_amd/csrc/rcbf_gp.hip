@@ -20,6 +20,7 @@
 // For the exact posterior R = L^-T is upper triangular and the column block
 // of logical columns [128 cb, 128 cb + 128) reads only training rows below
 // 128 (cb + 1): half the work of the dense product (RCBF_GP_RT_UPPER).
+#include <vector>
 #include "rcbf_common.hpp"
 
 using namespace rcbf;
@@ -982,13 +983,18 @@ int rcbf_gp_workspace_init(const rcbf_gp_model* m, float* workspace, hipStream_t
 int rcbf_gp_workspace_check(const rcbf_gp_model* m, float* workspace, hipStream_t stream) {
     if (!m || !workspace) return RCBF_E_NULL;
     if (m->C_pad < kGpCols || m->n_s < 1) return RCBF_E_BAD_SHAPE;
-    unsigned fail = 0;
-    int rc = (int)hipMemcpyAsync(&fail, reinterpret_cast<unsigned*>(workspace) + gp_fail_word(*m), 4,
-                                 hipMemcpyDeviceToHost, stream);
+    // every counter word and the fail word: once the stream has drained, a clean workspace reads all zero.  A
+    // set fail word is a call that drew a ticket past its counter's arrival count; a non-zero counter is a
+    // call whose counter started off by less than that (an early arrival took the "last" ticket, reset the
+    // counter, and the late ones left it non-zero without ever drawing a ticket past the count)
+    std::vector<unsigned> h((size_t)gp_counter_words(*m));
+    int rc = (int)hipMemcpyAsync(h.data(), workspace, h.size() * 4, hipMemcpyDeviceToHost, stream);
     if (!rc) rc = (int)hipStreamSynchronize(stream);
     if (rc) return rc;
-    if (!fail) return 0;
-    // the hand-off saw a non-zero counter: zero every counter and the fail word, so the next call is clean
+    bool bad = false;
+    for (unsigned v : h) bad |= v != 0;
+    if (!bad) return 0;
+    // zero every counter and the fail word, so the next call is clean
     rc = rcbf_gp_workspace_init(m, workspace, stream);
     if (!rc) rc = (int)hipStreamSynchronize(stream);
     return rc ? rc : RCBF_E_GP_HANDOFF;
@@ -1168,14 +1174,16 @@ int rcbf_gp_obs_safe_action(const rcbf_params* prm, const rcbf_gp_model* m, int6
     if (int rc = launch_status()) return rc;
     if (!done_word) return 0;
     // the result is on the host once the word reads `seq` (the kernel's last stage publishes it system-wide);
-    // every 4096 polls ask the stream, so a failed kernel returns its error instead of spinning
+    // every 4096 polls ask the stream, so a failed kernel returns its error instead of spinning.  A kernel
+    // that completed without publishing never reached its last stage: a hand-off counter was not zero at
+    // the start (the fail word is set; rcbf_gp_workspace_check reports and repairs it)
     volatile uint32_t* w = done_word;
     for (uint32_t n = 1;; ++n) {
         if (*w == seq) return 0;
         __builtin_ia32_pause();
         if ((n & 4095) == 0) {
             const hipError_t q = hipStreamQuery(stream);
-            if (q == hipSuccess) return *w == seq ? 0 : (int)hipErrorUnknown;
+            if (q == hipSuccess) return *w == seq ? 0 : RCBF_E_GP_HANDOFF;
             if (q != hipErrorNotReady) return (int)q;
         }
     }

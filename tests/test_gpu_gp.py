@@ -359,6 +359,45 @@ def test_gp_gemv_poisoned_counter_is_detected_and_reset(rank):
         assert torch.equal(m1, m2) and torch.equal(s1, s2)
 
 
+def test_one_launch_safe_action_reports_a_poisoned_counter():
+    """The one-launch select_action call (rcbf_gp_obs_safe_action) on a
+    workspace whose first arrival counter is far from zero: no workgroup draws
+    the last ticket, the kernel completes without publishing, and the call
+    returns RCBF_E_GP_HANDOFF instead of a stale action.  (A counter off by
+    less than the block's tile count makes an early arrival the "last" one:
+    that call's action is not valid, and only the fail word tells --
+    check_failures, run below after both kinds.)  check_failures reports the
+    fail word and zeroes the counters; the next call returns the clean action."""
+    import types
+    from rcbf_amd import gp
+    from rcbf_amd.diff_cbf_qp import CBFQPLayer
+    from rcbf_amd.envs import SimulatedCarsEnv
+    from rcbf_amd.sac_cbf import get_safe_action_host
+    rng = np.random.default_rng(21)
+    env = SimulatedCarsEnv()
+    layer = CBFQPLayer(env, types.SimpleNamespace(cuda=True), gamma_b=20.0)
+    tx, ty = _data(rng, 1500, 10)
+    hyper = [(rng.uniform(0.8, 2.5), rng.uniform(0.05, 0.5), rng.uniform(0.01, 0.2)) for _ in range(10)]
+    dm = types.SimpleNamespace(disturb_estimators=gp.GPDisturbanceModel(tx, ty, hyper, rank=100))
+    obs = torch.as_tensor(env.reset(), dtype=torch.float32, device="cuda")
+    u = torch.tensor([0.3], device="cuda")
+    clean = get_safe_action_host(layer, obs, u, dm)
+    gpm = dm.disturb_estimators
+    ws = gpm._sa_ws[2]
+    ws.view(torch.int32)[0] = 1 << 20
+    with pytest.raises(RuntimeError, match="RCBF_E_GP_HANDOFF"):
+        get_safe_action_host(layer, obs, u, dm)
+    with pytest.raises(RuntimeError, match="arrival counter"):
+        gpm.check_failures()
+    assert np.array_equal(get_safe_action_host(layer, obs, u, dm), clean)
+    ws.view(torch.int32)[0] = 3  # off by a few tiles: a premature "last" arrival, flagged by the fail word
+    get_safe_action_host(layer, obs, u, dm)
+    with pytest.raises(RuntimeError, match="arrival counter"):
+        gpm.check_failures()
+    assert np.array_equal(get_safe_action_host(layer, obs, u, dm), clean)
+    gpm.check_failures()
+
+
 def test_gp_workspace_per_stream():
     """GEMV calls on two streams at once use two
     workspaces (GPDisturbanceModel._workspace keys them by stream), so their
