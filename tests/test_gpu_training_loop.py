@@ -222,6 +222,8 @@ def _train(env_name, episodes, model_based):
             obs = next_obs
         rec["episodes"].append({"steps": ep_steps, "reward": ep_r, "cost": ep_c})
         rec["steps"] += ep_steps
+        if dm.disturb_estimators is not None:  # the GP hand-off's counters are clean after the episode
+            dm.disturb_estimators.check_failures()
     rec.update(fits=fits, agent=agent, dm=dm, memory_len=len(memory), memory_model_len=len(memory_model))
     return rec
 
