@@ -74,6 +74,10 @@ def parse():
     ap.add_argument("--rccl", action="store_true",
                     help="bring up the RCCL process group even on one rank: the N > 1 path's init, barriers, "
                          "all_gather and MAX all_reduce then run on the device (world size 1)")
+    ap.add_argument("--rehearse-shared-gpu", action="store_true",
+                    help="rehearsal of the N > 1 path on a 1-GPU box: every rank runs on GPU 0 (its own AQL queue and "
+                         "env shard), the process group is gloo; checks the multi-process launch, per-rank queues, "
+                         "barriers and max-over-ranks on the device path -- NOT a scaling measurement")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="CPU/gloo plumbing check of the launcher (no kernel, no measurement)")
     ap.add_argument("--launch", default=None, choices=["graph", "seq", "aql"],
@@ -663,13 +667,17 @@ def main():
         sync = lambda: None  # noqa: E731
     else:
         host_mask, host_cores = pin_host_cores(local, args.host_cores)
-        if local >= torch.cuda.device_count():
+        gpu = 0 if args.rehearse_shared_gpu else local
+        if gpu >= torch.cuda.device_count():
             raise SystemExit(f"rank {rank}: LOCAL_RANK {local}, but {torch.cuda.device_count()} HIP device(s) visible")
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
         if world > 1 or args.rccl:
             one_rank_rendezvous(world)
-            dist.init_process_group("nccl", device_id=dev)
+            if args.rehearse_shared_gpu:  # RCCL refuses two ranks on one GPU: the host-side group instead
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=dev)
         setup = setup_sac_update if args.workload == "sac_update" else setup_gpu
         env, layer, graph, S, active_frac, untimed, ctx = setup(args, dev, rank, B)
         reps = args.steps // S
@@ -715,9 +723,10 @@ def main():
         # dispatch timestamps of the same S steps, re-run profiled right after the timed region
         aql_times = aql_dispatch_times(env, layer, ctx, graph, S)
         kern_ms = aql_times["period_us"] / 1e3
-    per_rank_s = shard.gather_over_ranks(el, world, dev)
+    red_dev = torch.device("cpu") if args.rehearse_shared_gpu else dev  # gloo reduces host tensors
+    per_rank_s = shard.gather_over_ranks(el, world, red_dev)
     el = max(per_rank_s)
-    kern_ms = shard.max_over_ranks(kern_ms, world, dev)
+    kern_ms = shard.max_over_ranks(kern_ms, world, red_dev)
     value = shard.whole_job_rate(world, B, args.steps, el)
     bps = bytes_per_step(args)
     achieved = B * bps / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
@@ -819,6 +828,11 @@ def main():
                                      "(aql_dispatch_times.period_us; the AQL counterpart of HIP events around the "
                                      "region); host_submit_ms = host time of the timed run call (submission AND the "
                                      "wait for completion)")
+    if args.rehearse_shared_gpu:
+        rec["rehearsal"] = (f"{world} ranks sharing GPU 0 over a gloo group: a check of the N > 1 launch path, "
+                            "NOT a scaling measurement (the ranks contend for one GPU)")
+        rec["config"]["collectives"] = rec["config"]["collectives"] and rec["config"]["collectives"].replace(
+            "RCCL", "gloo")
     if world > 1:  # the spread of the timed region over ranks (value is set by the slowest)
         ms = sorted(v / args.steps * 1e3 for v in per_rank_s)
         rec["per_rank_ms"] = {"min": round(ms[0], 5), "median": round(float(np.median(ms)), 5),
