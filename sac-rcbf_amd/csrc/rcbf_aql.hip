@@ -432,52 +432,67 @@ int rcbf_aql_safe_step_plan(rcbf_aql* q, const rcbf_params* prm, int64_t B, int3
     return 0;
 }
 
-int rcbf_aql_run(rcbf_aql_plan* p, uint64_t timeout_us) {
-    if (!p || !p->q || !p->q->queue) return RCBF_E_NULL;
-    rcbf_aql* q = p->q;
-    if (q->queue_error.load()) return RCBF_E_HSA;
-    hsa_queue_t* queue = q->queue;
-    const uint32_t mask = queue->size - 1;
+}  // extern "C"
+
+namespace {
+
+// Copy packets j, j + 1, ... of plan p into its queue's ring, as many as the ring has room for right now,
+// and ring the doorbell once for them; returns the new j (unchanged when the ring is full).
+int32_t feed(rcbf_aql_plan* p, int32_t j) {
+    hsa_queue_t* queue = p->q->queue;
+    const uint64_t mask = queue->size - 1;
     auto* ring = static_cast<hsa_kernel_dispatch_packet_t*>(queue->base_address);
-    for (auto& s : p->sig) hsa_signal_store_relaxed(s, 1);
-    const uint64_t t_end = now_ns() + (timeout_us ? timeout_us : 10000000ull) * 1000ull;
-    int32_t j = 0;
-    while (j < p->K) {
-        // as many packets as the ring has room for (all of them unless K > the ring)
-        const uint64_t rd = hsa_queue_load_read_index_scacquire(queue);
-        const uint64_t wr = hsa_queue_load_write_index_relaxed(queue);
-        const uint64_t room = queue->size - (wr - rd);
-        if (room == 0) {
-            if (q->queue_error.load()) return RCBF_E_HSA;
-            if (now_ns() > t_end) return RCBF_E_TIMEOUT;
-            _mm_pause();
-            continue;
-        }
-        const int32_t n = (int32_t)std::min<uint64_t>(room, (uint64_t)(p->K - j));
-        const uint64_t w = hsa_queue_add_write_index_relaxed(queue, (uint64_t)n);
-        for (int32_t i = 0; i < n; ++i) {
-            hsa_kernel_dispatch_packet_t* slot = &ring[(w + i) & mask];
-            const hsa_kernel_dispatch_packet_t& src = p->pkt[j + i];
-            std::memcpy(reinterpret_cast<char*>(slot) + 4, reinterpret_cast<const char*>(&src) + 4,
-                        sizeof(src) - 4);
-            __atomic_store_n(reinterpret_cast<uint32_t*>(slot), (uint32_t)src.header | ((uint32_t)src.setup << 16),
-                             __ATOMIC_RELEASE);
-        }
-        hsa_signal_store_screlease(queue->doorbell_signal, (hsa_signal_value_t)(w + n - 1));
-        j += n;
+    const uint64_t rd = hsa_queue_load_read_index_scacquire(queue);
+    const uint64_t wr = hsa_queue_load_write_index_relaxed(queue);
+    const uint64_t room = queue->size - (wr - rd);
+    if (room == 0) return j;
+    const int32_t n = (int32_t)std::min<uint64_t>(room, (uint64_t)(p->K - j));
+    const uint64_t w = hsa_queue_add_write_index_relaxed(queue, (uint64_t)n);
+    for (int32_t i = 0; i < n; ++i) {
+        hsa_kernel_dispatch_packet_t* slot = &ring[(w + i) & mask];
+        const hsa_kernel_dispatch_packet_t& src = p->pkt[j + i];
+        std::memcpy(reinterpret_cast<char*>(slot) + 4, reinterpret_cast<const char*>(&src) + 4, sizeof(src) - 4);
+        __atomic_store_n(reinterpret_cast<uint32_t*>(slot), (uint32_t)src.header | ((uint32_t)src.setup << 16),
+                         __ATOMIC_RELEASE);
     }
-    // wait for the last packet's completion signal (busy wait: the host has
-    // nothing else to do in a synchronous step, and a sleeping wait adds its
-    // wake-up latency to every call)
+    hsa_signal_store_screlease(queue->doorbell_signal, (hsa_signal_value_t)(w + n - 1));
+    return j + n;
+}
+
+// Busy-wait for plan p's last completion signal (a synchronous step: the host has nothing else to do, and
+// a sleeping wait adds its wake-up latency to every call).
+int wait_done(rcbf_aql_plan* p, uint64_t t_end) {
     const hsa_signal_t last = p->sig.back();
     for (;;) {
         const hsa_signal_value_t v =
             hsa_signal_wait_scacquire(last, HSA_SIGNAL_CONDITION_LT, 1, 1000000, HSA_WAIT_STATE_ACTIVE);
-        if (v < 1) break;
-        if (q->queue_error.load()) return RCBF_E_HSA;
+        if (v < 1) return p->q->queue_error.load() ? RCBF_E_HSA : 0;
+        if (p->q->queue_error.load()) return RCBF_E_HSA;
         if (now_ns() > t_end) return RCBF_E_TIMEOUT;
     }
-    return q->queue_error.load() ? RCBF_E_HSA : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rcbf_aql_run(rcbf_aql_plan* p, uint64_t timeout_us) {
+    if (!p || !p->q || !p->q->queue) return RCBF_E_NULL;
+    if (p->q->queue_error.load()) return RCBF_E_HSA;
+    for (auto& s : p->sig) hsa_signal_store_relaxed(s, 1);
+    const uint64_t t_end = now_ns() + (timeout_us ? timeout_us : 10000000ull) * 1000ull;
+    // as many packets as the ring has room for (all of them unless K > the ring), then the rest as the
+    // packet processor frees slots
+    for (int32_t j = 0; j < p->K;) {
+        const int32_t nj = feed(p, j);
+        if (nj == j) {
+            if (p->q->queue_error.load()) return RCBF_E_HSA;
+            if (now_ns() > t_end) return RCBF_E_TIMEOUT;
+            _mm_pause();
+        }
+        j = nj;
+    }
+    return wait_done(p, t_end);
 }
 
 int rcbf_aql_plan_times(const rcbf_aql_plan* p, uint64_t* start_end_ns) {
