@@ -8,6 +8,7 @@ its slack-violation warning (:283-284) is: any row whose slack |epsilon|
 exceeds 0.1 prints the reference's message (get_u_safe and solve_qp).
 """
 import ctypes
+import threading
 import weakref
 
 import numpy as np
@@ -81,6 +82,9 @@ class CascadeCBFLayer:
         X = np.atleast_2d(np.asarray(s, np.float64))
         B, n_u = U.shape
         n_s = X.shape[1]
+        dims = DYNAMICS_MODE[self.env.dynamics_mode]
+        if X.shape[0] != B or n_s != dims["n_s"] or n_u != dims["n_u"]:
+            raise ValueError(f"expected u_nom (B, {dims['n_u']}) and state (B, {dims['n_s']}), got {U.shape} / {X.shape}")
         st = self._staging(B, n_s, n_u)
         st["u"][:B * n_u] = U.reshape(-1)
         st["x"][:B * n_s] = X.reshape(-1)
@@ -102,8 +106,12 @@ class CascadeCBFLayer:
     def _staging(self, B, n_s, n_u):
         """A pinned host block (rcbf_host_alloc) of _SYNC_MAX_B samples: u_nom,
         state, mean, sigma, u_safe, epsilon (f64), status (i32), the completion
-        word; numpy views over it."""
-        st = self.__dict__.get("_stage")
+        word; numpy views over it.  One block per calling thread: two threads
+        calling get_u_safe on one layer at once must not share a completion
+        word."""
+        stages = self.__dict__.setdefault("_stages", {})
+        tid = threading.get_ident()
+        st = stages.get(tid)
         if st is not None:
             return st
         cap = _SYNC_MAX_B
@@ -122,8 +130,8 @@ class CascadeCBFLayer:
                 st[name] = np.ctypeslib.as_array((ctypes.c_double * (b // 8)).from_address(a))
             off += -(-b // 64) * 64
         ctypes.c_uint32.from_address(st["pw"]).value = 0
-        self._stage = st
-        self._stage_fin = weakref.finalize(self, _lib.load().rcbf_host_free, ptr.value)
+        stages[tid] = st
+        st["fin"] = weakref.finalize(self, _lib.load().rcbf_host_free, ptr.value)
         return st
 
     def get_cbf_qp_constraints(self, u_nom, state, mean_pred, sigma_pred):

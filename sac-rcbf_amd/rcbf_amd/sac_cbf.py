@@ -18,6 +18,7 @@ safe action in one kernel) writes the action into pinned host memory and a
 completion word, so no device-to-host copy or stream synchronisation follows.
 """
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -68,7 +69,7 @@ def get_safe_action(cbf_layer, obs_batch, action_batch, dynamics_model):
 
 
 class _HostSlot:
-    """A pinned host block per device for rcbf_gp_obs_safe_action: the action
+    """A pinned host block per device and thread for rcbf_gp_obs_safe_action: the action
     (<= 2 floats) at byte 0, the QP status at byte 32, the completion word at
     byte 64 (its own line)."""
 
@@ -104,9 +105,12 @@ def _ready(t, dev):
 
 
 def _slot(dev):
-    s = _SLOTS.get(dev.index)
+    """The calling thread's host slot on `dev` (two threads must not share a
+    completion word)."""
+    key = (dev.index, threading.get_ident())
+    s = _SLOTS.get(key)
     if s is None:
-        s = _SLOTS[dev.index] = _HostSlot()
+        s = _SLOTS[key] = _HostSlot()
     return s
 
 
