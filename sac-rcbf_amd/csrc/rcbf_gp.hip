@@ -939,8 +939,11 @@ __global__ void __launch_bounds__(256) k_gp_finish_cols(rcbf_gp_model m, int64_t
 
 // Split-K factor: 1 when the (query tile x column block x GP) grid already
 // gives every CU several workgroups; otherwise enough splits of the training
-// rows for ~6 workgroups per CU (3 resident per CU at 160 VGPRs), each split
-// at least one 256-row LDS chunk.
+// rows for ~6 workgroups per CU (3 resident per CU at 160 VGPRs), capped at one
+// split per 256-row LDS chunk, the last chunk counted even when partial: rank
+// 100 at N = 3 000, B = 256 then runs 12 splits of 256 rows (240 workgroups,
+// 8 blocks of 32 rows each) instead of 11 of 288 (9 blocks): 39.2 -> 36.4 us
+// (profiles/r06/gp_split_sweep_r06t.txt).
 constexpr int kGvMaxB = 8;  // B <= 8: the streaming GEMV path
 
 int gp_split(const rcbf_gp_model* m, int64_t B) {
@@ -953,7 +956,7 @@ int gp_split(const rcbf_gp_model* m, int64_t B) {
     const int64_t want = 6LL * cus;
     if (tiles >= want / 2) return 1;
     int64_t sk = (want + tiles - 1) / tiles;
-    const int64_t cap = m->N_pad / kGpChunk;
+    const int64_t cap = (m->N_pad + kGpChunk - 1) / kGpChunk;
     sk = sk < cap ? sk : cap;
     return sk < 1 ? 1 : (int)sk;
 }

@@ -146,7 +146,7 @@ for step in "$@"; do
     loop)   run loop 900 python -u -m pytest tests/test_gpu_training_loop.py -q -rf -s --timeout 600 --timeout-method thread ;;
     gpgb)   run gpgb 300 python -u scripts/gp_graph_bench.py ;;
     gpsk)   # split-K count sweep of the B = 256 GP posterior (study build build/variants/librcbf_gpsplit.so)
-      for sk in 0 6 11 16 22 32 47; do
+      for sk in ${GPSK_LIST:-0 6 11 16 22 32 47}; do
         if [ "$sk" = 0 ]; then e=""; else e="RCBF_GP_SPLIT=$sk"; fi
         env $e RCBF_HIP_LIB=build/variants/librcbf_gpsplit.so GP_BENCH_ONLY=love100:256 timeout -k 10 200 \
           python scripts/gp_graph_bench.py 20 5 > "$OUT/gpsk_$sk.log" 2>&1 || exit 1
