@@ -110,3 +110,26 @@ def test_rccl_flag_brings_up_the_group_on_one_rank():
                         "--warmup", "1", "--batch", "256"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["config"]["collectives"] is None
+
+
+def test_committed_roofline_records_recompute():
+    """every committed roofline record (bench.py --record) recomputes its own figures --
+    frac from bytes_per_launch and kernel_us_per_step, frac_wall from ms_per_step, the per-step GPU time as the
+    median of its dispatch-timestamp runs -- and nests as an untraced run must: in-kernel span <= per-step GPU
+    time <= wall time per step.  bench.py finds the driver-form record for the driver's command."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "roofline_record_*.json")))
+    assert paths
+    for p in paths:
+        r = json.load(open(p))
+        k_us, wall_us = r["kernel_us_per_step"], r["ms_per_step"] * 1e3
+        frac = r["bytes_per_launch"] / (k_us * 1e-6) / 1e9 / r["peak_GBs"]
+        assert abs(frac - r["frac"]) <= 0.002, p
+        assert abs(r["bytes_per_launch"] / (wall_us * 1e-6) / 1e9 / r["peak_GBs"] - r["frac_wall"]) <= 0.002, p
+        runs = r["aql_dispatch_times"]["runs"]
+        periods = sorted((x["last_end_ns"] - x["first_start_ns"]) / 1e3 / r["steps"] for x in runs)
+        assert abs(periods[len(periods) // 2] - k_us) <= 0.01, p
+        assert r["span"]["kernel_span_us_median"] <= k_us <= wall_us + 0.01, p
+        assert r["bytes_per_launch"] == r["batch"] * r["bytes_per_env_step"]
+    k_us, src = bench.roofline_record("cars", 65536, "driver", "aql")
+    assert src and "driver_form" in src and 2.0 < k_us < 6.0
