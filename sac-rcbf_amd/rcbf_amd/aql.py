@@ -115,6 +115,9 @@ class AqlPlan:
         """Submit the K steps and return when they have completed."""
         if sync_hip:
             torch.cuda.synchronize(self.queue.device)
+        if not self._fin.alive:
+            raise RuntimeError("the AQL plan was freed")
+        # ctypes, not the CPython binding: a 20-step run measured the same through both (85.1 / 85.5 us, r06w)
         _check(_lib.load().rcbf_aql_run(self._h, timeout_us), "rcbf_aql_run")
         return self._env.obs, self._keep[2]["reward"], self._keep[2]["done"], self._keep[2]
 
