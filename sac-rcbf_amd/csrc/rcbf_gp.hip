@@ -47,6 +47,11 @@ constexpr int gp_chunk() { return SK ? RCBF_GP_SK_CHUNK : kGpChunk; }
 // LDS (gp_qform_dot_staged).  0: the earlier loop, kept for A/B builds: D VALU
 // FMAs per A value and every wave loading its own B values.
 constexpr bool kGpDot = RCBF_GP_DOT_MFMA != 0;
+// 1: split-K launches k_gp_qform_sk2 (two wave groups, 512 threads); 0: k_gp_qform<D, 4, true> (256 threads)
+#ifndef RCBF_GP_SK2
+#define RCBF_GP_SK2 1
+#endif
+constexpr bool kGpSk2 = RCBF_GP_SK2 != 0 && kGpDot;
 constexpr int kGpRtBuf = kGpDot ? 2 * 32 * kGpCols : 1;  // floats: two 32-row slices of the column block
 template <int D>
 struct GpAug {
@@ -89,7 +94,11 @@ __device__ __forceinline__ void gp_query_operand(const float (&xs2)[D], float q0
 // (16 B per lane, lane-linear: one wave-instruction = 2 rows) while block
 // bg - 1 is computed; one barrier per block.  The k-step r B value of lane
 // (l32, half) is then a ds_read_b128 of row 8 g + 4 half + j.
-template <int D, bool SK, bool HAS_MEAN>
+// G = 2 (the split-K instantiation, 512 threads): two groups of 4 waves share the workgroup's query rows
+// and take alternate 32-row blocks (group g: blocks 2 it + g), two waves per SIMD, so one wave's LDS reads,
+// exp2 and barrier waits overlap the other's MFMAs; the groups' accumulators are added through LDS after
+// the loop (gp_qform_body).
+template <int D, bool SK, bool HAS_MEAN, int G = 1>
 __device__ __forceinline__ void gp_qform_dot_staged(const rcbf_gp_model& m, int i, int cb, int n_beg, int n_end,
                                                     const float (&xs2)[D], float q0, float log2s, const float* alpha_i,
                                                     const float* xt_i, const float* tn2_i, int64_t ldc, int half,
@@ -99,22 +108,32 @@ __device__ __forceinline__ void gp_qform_dot_staged(const rcbf_gp_model& m, int 
     constexpr float kL2E = 1.4426950408889634f;
     float* s_ta = reinterpret_cast<float*>(s_xt);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int grp = G == 1 ? 0 : w >> 2;  // wave group: blocks 2 it + grp
     float qb[A::KS];
     gp_query_operand<D>(xs2, q0, half, qb);
     const float* Rt_cb = m.Rt + (int64_t)i * m.N_pad * ldc + (int64_t)cb * kGpCols;  // this column block
-    auto issue_rt = [&](int bg) {  // block bg of the range -> buffer bg & 1
-        float* buf = s_rt + (bg & 1) * 32 * kGpCols;
+    const int nb = (n_end - n_beg) / 32;  // N_pad and the split bounds are multiples of 32
+    // G = 1: block bg -> buffer bg & 1.  G = 2: iteration it stages blocks 2 it, 2 it + 1 into buffers
+    // 2 (it & 1), 2 (it & 1) + 1 (every thread copies 16 B of 4 slots of the 2 x 16 KB)
+    auto issue_rt = [&](int it) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = (q * 4 + w) * 64 + lane;  // float4 index in the 32 x 32 float4 image
-            const float* src = Rt_cb + (int64_t)(n_beg + 32 * bg + (e >> 5)) * ldc + 4 * (e & 31);
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)(buf + (q * 4 + w) * 256),
-                                             16, 0, 0);
+        for (int gb = 0; gb < G; ++gb) {
+            const int bg = G * it + gb;
+            if (bg >= nb) break;
+            float* buf = s_rt + (G * (it & 1) + gb) * 32 * kGpCols;
+#pragma unroll
+            for (int q = 0; q < 4 / G; ++q) {
+                const int slot = q * (4 * G) + w;          // 64-lane slot of the 32 x 32 float4 image
+                const int e = slot * 64 + lane;            // float4 index in it
+                const float* src = Rt_cb + (int64_t)(n_beg + 32 * bg + (e >> 5)) * ldc + 4 * (e & 31);
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                                 (__attribute__((address_space(3))) void*)(buf + slot * 256),
+                                                 16, 0, 0);
+            }
         }
     };
     auto stage_ta = [&](int n0, int nch) {
-        for (int e = threadIdx.x; e < nch; e += 256) {
+        for (int e = threadIdx.x; e < nch; e += 256 * G) {
             float ta[A::KA];
             ta[0] = 1.0f;
             ta[1] = -kL2E * tn2_i[n0 + e];
@@ -127,20 +146,23 @@ __device__ __forceinline__ void gp_qform_dot_staged(const rcbf_gp_model& m, int 
             if constexpr (HAS_MEAN) s_alpha[e] = alpha_i[(int64_t)(n0 + e) * ldc];
         }
     };
-    const int nb = (n_end - n_beg) / 32;  // N_pad and the split bounds are multiples of 32
+    const int nit = (nb + G - 1) / G;
     if (nb > 0) issue_rt(0);
 #pragma unroll 1
-    for (int bg = 0; bg < nb; ++bg) {
-        const int lb = bg % (gp_chunk<SK>() / 32);  // block within the staged chunk of training rows
-        if (lb == 0) {  // a new chunk of training rows: every wave done with the previous one first
+    for (int it = 0; it < nit; ++it) {
+        const int bg = G * it + grp;  // this wave's block
+        const int lb0 = (G * it) % (gp_chunk<SK>() / 32);  // the iteration's first block within its chunk
+        if (lb0 == 0) {  // a new chunk of training rows: every wave done with the previous one first
             __syncthreads();
-            stage_ta(n_beg + 32 * bg, min(gp_chunk<SK>(), n_end - (n_beg + 32 * bg)));
+            stage_ta(n_beg + 32 * G * it, min(gp_chunk<SK>(), n_end - (n_beg + 32 * G * it)));
         }
-        // ONE barrier per block: its vmcnt(0) retires this wave's copy of block bg, and past it every
-        // wave has finished block bg - 1, so its buffer ((bg + 1) & 1) is free for block bg + 1
+        // ONE barrier per iteration: its vmcnt(0) retires this wave's copies of iteration it, and past it
+        // every wave has finished iteration it - 1, so its buffers are free for iteration it + 1
         __syncthreads();
-        if (bg + 1 < nb) issue_rt(bg + 1);
-        const float* buf = s_rt + (bg & 1) * 32 * kGpCols;
+        if (it + 1 < nit) issue_rt(it + 1);
+        if (bg >= nb) continue;  // G = 2, odd block count: the second group sits out the last iteration
+        const int lb = lb0 + grp;
+        const float* buf = s_rt + (G * (it & 1) + grp) * 32 * kGpCols;
         const float* tp = s_ta + (lb * 32 + l32) * 2 * A::KSP + half * A::KSP;
         float af[A::KS];
 #pragma unroll
@@ -192,7 +214,7 @@ __device__ __forceinline__ void gp_qform_dot_staged(const rcbf_gp_model& m, int 
 // the epilogue.  One v_fma_f64 per k-step beside four MFMAs.
 // MEAN: this workgroup's column block holds the mean column r (a separate
 // instantiation, so the other ~95 % of the workgroups run the plain loop).
-template <int D, int CT, bool SK, bool MEAN>
+template <int D, int CT, bool SK, bool MEAN, int G = 1>
 __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B, const float* __restrict__ xq,
                                               float* __restrict__ partial, float* __restrict__ meanraw, int n_split,
                                               float* __restrict__ qraw, float4* s_xt, float* s_tn, float* s_alpha,
@@ -210,8 +232,10 @@ __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B,
     const int cb = blockIdx.y / (4 / CT);          // 128-column block
     const int sub = blockIdx.y % (4 / CT);         // which CT tiles of it
     const int n_part = gridDim.y;
+    static_assert(G == 1 || (G == 2 && SK && kGpDot), "two wave groups: the split-K MFMA-argument path only");
     const int64_t b0 = (int64_t)blockIdx.x * kGpRows;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = (threadIdx.x >> 6) & 3;  // w: the wave's 32 query rows
+    const int grp = G == 1 ? 0 : (int)(threadIdx.x >> 8);           // wave group (G = 2)
     const int half = lane >> 5, l32 = lane & 31;
     const float sl = m.inv_sl[i];
     const float log2s = __log2f(m.outscale[i]);
@@ -267,8 +291,26 @@ __device__ __forceinline__ void gp_qform_body(const rcbf_gp_model& m, int64_t B,
     const float* alpha_i = m.Rt + (int64_t)i * m.N_pad * ldc + alpha_phys;
     double macc = 0.0;
     if constexpr (kGpDot) {
-        gp_qform_dot_staged<D, SK, has_mean>(m, i, cb, n_beg, n_end, xs2, q0, log2s, alpha_i, xt_i, tn2_i, ldc, half,
-                                             l32, acc, macc, s_xt, s_alpha, s_rt);
+        gp_qform_dot_staged<D, SK, has_mean, G>(m, i, cb, n_beg, n_end, xs2, q0, log2s, alpha_i, xt_i, tn2_i, ldc,
+                                                half, l32, acc, macc, s_xt, s_alpha, s_rt);
+        if constexpr (G == 2) {  // group 1 hands its accumulators to group 0 through LDS (the staging buffers)
+            __syncthreads();
+            // element-major: register (c, r) of the 256 lanes of a group is one contiguous row of 256 floats,
+            // so every LDS access is lane-consecutive (no bank conflicts); 64 KB = the four staging buffers
+            float* xa = s_rt + w * 64 + lane;
+            if (grp == 1) {
+#pragma unroll
+                for (int c = 0; c < CT; ++c)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) xa[(c * 16 + r) * 256] = acc[c][r];
+            }
+            __syncthreads();
+            if (grp == 1) return;
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[c][r] += xa[(c * 16 + r) * 256];
+        }
     } else
     for (int n0 = n_beg; n0 < n_end; n0 += kGpChunk) {
         const int nch = min(kGpChunk, n_end - n0);  // multiple of 32
@@ -382,6 +424,20 @@ __global__ void __launch_bounds__(256) k_gp_qform(rcbf_gp_model m, int64_t B, co
         gp_qform_body<D, CT, SK, true>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha, s_rt);
     else
         gp_qform_body<D, CT, SK, false>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha, s_rt);
+}
+
+// The split-K instantiation with two wave groups (G = 2, 512 threads): each 128-query workgroup runs 8
+// waves, two per SIMD, over alternate 32-row blocks of its split (gp_qform_dot_staged), four staging
+// buffers (64 KB, reused for the groups' accumulator hand-off).
+template <int D>
+__global__ void __launch_bounds__(512) k_gp_qform_sk2(rcbf_gp_model m, int64_t B, const float* __restrict__ xq,
+                                                      float* __restrict__ partial, float* __restrict__ meanraw,
+                                                      int n_split, float* __restrict__ qraw) {
+    __shared__ float4 s_xt[gp_chunk<true>() * GpAug<D>::F4];
+    __shared__ float s_tn[1];
+    __shared__ float s_alpha[1];
+    __shared__ __attribute__((aligned(16))) float s_rt[2 * kGpRtBuf];
+    gp_qform_body<D, 4, true, false, 2>(m, B, xq, partial, meanraw, n_split, qraw, s_xt, s_tn, s_alpha, s_rt);
 }
 
 // Few queries (B <= 8, the per-env-step query of main.py, B = 1): the
@@ -1079,7 +1135,10 @@ int rcbf_gp_predict_cols(const rcbf_gp_model* m, int64_t B, const float* x, floa
         dim3 g((unsigned)((B + kGpRows - 1) / kGpRows), (unsigned)n_part, (unsigned)(m->n_s * sk));
 #define RCBF_GP_L(DD)                                                                                           \
     do {                                                                                                        \
-        if (sk > 1)                                                                                             \
+        if (sk > 1 && kGpSk2)                                                                                   \
+            hipLaunchKernelGGL((k_gp_qform_sk2<DD>), g, dim3(512), 0, stream, *m, B, x, partial, meanraw, sk,   \
+                               qraw);                                                                           \
+        else if (sk > 1)                                                                                        \
             hipLaunchKernelGGL((k_gp_qform<DD, 4, true>), g, dim3(256), 0, stream, *m, B, x, partial, meanraw, \
                                sk, qraw);                                                                       \
         else                                                                                                    \
