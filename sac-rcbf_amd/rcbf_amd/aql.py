@@ -47,6 +47,7 @@ class AqlQueue:
         _check(lib.rcbf_aql_open(self.device.index, code_object.encode() if code_object else None,
                                  PROFILE if profile else 0, ctypes.byref(h)), "rcbf_aql_open")
         self._h = h
+        self._plans = weakref.WeakSet()  # live plans: freed before the queue (they point into it)
         self._fin = weakref.finalize(self, lib.rcbf_aql_close, h)
 
     @property
@@ -59,6 +60,8 @@ class AqlQueue:
         return int(_lib.load().rcbf_aql_kernel_count(self.handle))
 
     def close(self):
+        for p in list(self._plans):
+            p.free()
         self._fin()
 
     def safe_step_plan(self, env, u_rl_seq, layer, steps=None, mean=None, sigma=None, outputs=None,
@@ -100,7 +103,9 @@ class AqlQueue:
                 (PROFILE if profile else 0) | int(fence_flags), ctypes.byref(h)), "rcbf_aql_safe_step_plan")
         # the plan holds raw pointers: keep every tensor it reads or writes alive with it
         keep = (env, layer, o, us, mean, sigma, span)
-        return AqlPlan(self, h, K, keep, bool(profile), env)
+        plan = AqlPlan(self, h, K, keep, bool(profile), env)
+        self._plans.add(plan)
+        return plan
 
 
 class AqlPlan:
@@ -115,8 +120,8 @@ class AqlPlan:
         """Submit the K steps and return when they have completed."""
         if sync_hip:
             torch.cuda.synchronize(self.queue.device)
-        if not self._fin.alive:
-            raise RuntimeError("the AQL plan was freed")
+        if not self._fin.alive or not self.queue._fin.alive:
+            raise RuntimeError("the AQL plan (or its queue) was freed")
         # ctypes, not the CPython binding: a 20-step run measured the same through both (85.1 / 85.5 us, r06w)
         _check(_lib.load().rcbf_aql_run(self._h, timeout_us), "rcbf_aql_run")
         return self._env.obs, self._keep[2]["reward"], self._keep[2]["done"], self._keep[2]
@@ -125,6 +130,8 @@ class AqlPlan:
         """(K, 2) int64 numpy array: each dispatch's start and end (ns, HSA
         system clock) from the last run; profiled plans only."""
         import numpy as np
+        if not self._fin.alive:
+            raise RuntimeError("the AQL plan was freed")
         out = np.zeros((self.K, 2), dtype=np.uint64)
         _check(_lib.load().rcbf_aql_plan_times(self._h, out.ctypes.data), "rcbf_aql_plan_times")
         return out.astype(np.int64)

@@ -135,6 +135,25 @@ def test_profiled_plan_times_and_span(queue):
     e2.check_failures()
 
 
+def test_closing_the_queue_frees_its_plans():
+    """A plan points into its queue: AqlQueue.close() frees the live plans
+    first, and a freed plan (or one whose queue is closed) refuses to run
+    instead of touching freed memory."""
+    from rcbf_amd.aql import AqlQueue
+    (e1, l1), _ = _pair("SimulatedCars", 256)
+    q = AqlQueue(torch.device("cuda", 0))
+    pool = [torch.zeros(256, 1, device="cuda")]
+    p1 = q.safe_step_plan(e1, pool, l1, steps=2)
+    p2 = q.safe_step_plan(e1, pool, l1, steps=3)
+    p1.run()
+    p2.free()
+    with pytest.raises(RuntimeError, match="freed"):
+        p2.run()
+    q.close()
+    with pytest.raises(RuntimeError, match="freed"):
+        p1.run()
+
+
 def test_plan_argument_errors(queue):
     (e1, l1), _ = _pair("SimulatedCars", 256)
     pool = [torch.zeros(256, 1, device="cuda")]
