@@ -542,7 +542,9 @@ int rcbf_safe_rollout(const rcbf_params* prm, int64_t B, int32_t K, double* x, d
  * RCBF_AQL_PROFILE_ENDS: on the first and last dispatch only (the others
  * read back as 0).
  * rcbf_aql_run: submit the K dispatches (barrier bit on each), ring the
- * doorbell once, busy-wait for completion; timeout_us 0 -> 10 s.
+ * doorbell once, busy-wait for completion; timeout_us 0 -> 10 s.  A plan
+ * must not run after rcbf_aql_close of its queue (rcbf_aql_plan_free may
+ * still be called then).
  * Returns RCBF_E_HSA / RCBF_E_TIMEOUT on a queue error or a timeout. */
 #define RCBF_AQL_PROFILE 1
 /* plan flags: memory-fence scopes (default: agent scope everywhere but the

@@ -123,6 +123,7 @@ struct rcbf_aql {
 
 struct rcbf_aql_plan {
     rcbf_aql* q = nullptr;
+    int device = -1;  // the queue's HIP device (rcbf_aql_plan_free does not read q: a plan may outlive it)
     int32_t K = 0;
     void* kernargs = nullptr;                       // K * kArgStride bytes of device memory
     std::vector<hsa_kernel_dispatch_packet_t> pkt;  // pre-built packets (header written last, atomically)
@@ -353,6 +354,7 @@ int rcbf_aql_safe_step_plan(rcbf_aql* q, const rcbf_params* prm, int64_t B, int3
 
     auto* p = new rcbf_aql_plan();
     p->q = q;
+    p->device = q->device;
     p->K = K;
     p->profiled = ends ? 2 : profiled ? 1 : 0;
     std::vector<unsigned char> host((size_t)K * kArgStride, 0);
@@ -519,7 +521,7 @@ int rcbf_aql_plan_times(const rcbf_aql_plan* p, uint64_t* start_end_ns) {
 int rcbf_aql_plan_free(rcbf_aql_plan* p) {
     if (!p) return 0;
     if (p->kernargs) {
-        DeviceGuard guard(p->q->device);
+        DeviceGuard guard(p->device);
         (void)hipFree(p->kernargs);
     }
     for (auto& s : p->sig) hsa_signal_destroy(s);
