@@ -130,8 +130,8 @@ class AqlPlan:
         """(K, 2) int64 numpy array: each dispatch's start and end (ns, HSA
         system clock) from the last run; profiled plans only."""
         import numpy as np
-        if not self._fin.alive:
-            raise RuntimeError("the AQL plan was freed")
+        if not self._fin.alive or not self.queue._fin.alive:
+            raise RuntimeError("the AQL plan (or its queue) was freed")
         out = np.zeros((self.K, 2), dtype=np.uint64)
         _check(_lib.load().rcbf_aql_plan_times(self._h, out.ctypes.data), "rcbf_aql_plan_times")
         return out.astype(np.int64)
