@@ -135,6 +135,27 @@ def test_profiled_plan_times_and_span(queue):
     e2.check_failures()
 
 
+def test_one_step_plan_over_a_persistent_action_buffer(queue):
+    """INTEGRATION.md's training-loop form: a one-step plan over a buffer the
+    policy rewrites every step (torch writes it on its stream; run() waits for
+    that work first).  30 steps equal 30 safe_step launches bit for bit."""
+    B = 4096
+    (e1, l1), (e2, l2) = _pair("Unicycle", B, hazards=5)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(4)
+    acts = [(torch.rand(B, 2, device="cuda", generator=gen) * 2 - 1).contiguous() for _ in range(30)]
+    o1, o2 = e1.make_outputs(), e2.make_outputs()
+    u_buf = torch.zeros(B, 2, device="cuda")
+    step1 = queue.safe_step_plan(e2, [u_buf], l2, steps=1, outputs=o2)
+    for a in acts:
+        e1.safe_step(a, l1, outputs=o1)
+        u_buf.copy_(a)
+        step1.run()
+    torch.cuda.synchronize()
+    _assert_same(_snapshot(e1, o1), _snapshot(e2, o2))
+    step1.free()
+
+
 def test_closing_the_queue_frees_its_plans():
     """A plan points into its queue: AqlQueue.close() frees the live plans
     first, and a freed plan (or one whose queue is closed) refuses to run
